@@ -1,0 +1,662 @@
+// rtx_capi.hip — C ABI (include/rtx.h) over the HIP kernels: scene upload, IntersectBatch,
+// full-path render.  gfx950 only; no CPU compute path and no fallback: a missing device or a
+// HIP error is returned as RTX_ERR_* with a message in rtx_last_error().
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "rtx.h"
+#include "rtx_kernels.h"
+
+using namespace rtxd;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPC(expr)                                                                                   \
+  do {                                                                                               \
+    hipError_t e_ = (expr);                                                                          \
+    if (e_ != hipSuccess)                                                                            \
+      return fail(RTX_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_) + " (" __FILE__ ":" + \
+                                   std::to_string(__LINE__) + ")");                                  \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  int reserve(size_t bytes) {
+    if (bytes <= n) return RTX_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr, n = 0;
+    if (bytes == 0) return RTX_OK;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) return fail(RTX_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    n = bytes;
+    return RTX_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr, n = 0;
+  }
+  template <class T>
+  T* as() const {
+    return (T*)p;
+  }
+};
+
+float round_down(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = std::nextafter(f, -INFINITY);
+  return f;
+}
+float round_up(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = std::nextafter(f, INFINITY);
+  return f;
+}
+
+}  // namespace
+
+struct rtx_scene {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int cus = 0;
+  DevBuf nodes, prims, mats, texs, images, fnodes;
+  std::vector<DevBuf> texels;
+  DScene S{};
+  int stack_parity = 32, stack_fast = 32;
+  int64_t n_nodes = 0;
+  // render workspace (grow-only)
+  DevBuf px_sum, px_mean, px_m2, px_samples, px_conv, lbuf, queue[2], counters, out_rgb, out_spp, rays, hits;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  std::vector<hipEvent_t> evpool;
+  ~rtx_scene() {
+    for (auto e : evpool) (void)hipEventDestroy(e);
+    (void)hipSetDevice(device);
+    for (DevBuf* b : {&nodes, &prims, &mats, &texs, &images, &fnodes, &px_sum, &px_mean, &px_m2, &px_samples,
+                      &px_conv, &lbuf, &queue[0], &queue[1], &counters, &out_rgb, &out_spp, &rays, &hits})
+      b->release();
+    for (auto& t : texels) t.release();
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace {
+
+// Tree depth of the reference-layout BVH (pre-order, left = idx+1).
+int bvh_depth(const rtx_bvh_node* n, int64_t count) {
+  if (count == 0) return 0;
+  std::vector<int> d(count, 0);
+  int m = 1;
+  for (int64_t i = 0; i < count; i++) {
+    m = std::max(m, d[i] + 1);
+    if (!n[i].is_leaf) {
+      d[n[i].left_first] = d[i] + 1;
+      d[n[i].right_count] = d[i] + 1;
+    }
+  }
+  return m;
+}
+
+// BVH2 fast layout: one FNode per internal node, holding both children's outward-rounded
+// f32 boxes (see rtx_device.h FNode / fbox).
+void build_fast(const rtx_bvh_node* n, int64_t count, std::vector<FNode>& out) {
+  std::vector<int32_t> fidx(count, -1);
+  int32_t k = 0;
+  for (int64_t i = 0; i < count; i++)
+    if (!n[i].is_leaf) fidx[i] = k++;
+  out.assign(k, FNode{});
+  for (int64_t i = 0; i < count; i++) {
+    if (n[i].is_leaf) continue;
+    FNode& f = out[fidx[i]];
+    const uint32_t ch[2] = {n[i].left_first, n[i].right_count};
+    for (int c = 0; c < 2; c++) {
+      const rtx_bvh_node& cn = n[ch[c]];
+      float* lo = c == 0 ? f.lo0 : f.lo1;
+      float* hi = c == 0 ? f.hi0 : f.hi1;
+      for (int a = 0; a < 3; a++) lo[a] = round_down(cn.lo[a]), hi[a] = round_up(cn.hi[a]);
+      int32_t ref;
+      uint16_t cnt;
+      if (cn.is_leaf) ref = ~(int32_t)cn.left_first, cnt = (uint16_t)cn.right_count;
+      else ref = fidx[ch[c]], cnt = 0;
+      if (c == 0) f.c0 = ref, f.n0 = cnt;
+      else f.c1 = ref, f.n1 = cnt;
+    }
+  }
+}
+
+int pick_stack(int depth) {
+  if (depth + 2 <= 32) return 32;
+  if (depth + 2 <= 64) return 64;
+  return -1;
+}
+
+template <class T>
+int upload(DevBuf& b, const T* src, size_t n, hipStream_t s) {
+  int rc = b.reserve(std::max<size_t>(n * sizeof(T), 16));
+  if (rc) return rc;
+  if (n) HIPC(hipMemcpyAsync(b.p, src, n * sizeof(T), hipMemcpyHostToDevice, s));
+  return RTX_OK;
+}
+
+int64_t subset_pixels(const rtx_camera* cam, const rtx_render_params* p, PixelMap& m, std::string& err) {
+  m.W = cam->image_width, m.H = cam->image_height;
+  if (m.W <= 0 || m.H <= 0) {
+    err = "camera not initialised (image size <= 0)";
+    return -1;
+  }
+  if (p->stripe_rows > 0) {
+    if (p->stripe_count <= 0 || p->stripe_index < 0 || p->stripe_index >= p->stripe_count) {
+      err = "bad stripe_index/stripe_count";
+      return -1;
+    }
+    m.stripes = 1, m.srows = p->stripe_rows, m.sidx = p->stripe_index, m.scount = p->stripe_count;
+    int64_t rows = 0;
+    for (int y = 0; y < m.H; y++)
+      if ((y / m.srows) % m.scount == m.sidx) rows++;
+    m.x0 = m.y0 = 0, m.w = m.W, m.h = (int)rows;
+    return rows * (int64_t)m.W;
+  }
+  m.stripes = 0;
+  m.x0 = p->x0, m.y0 = p->y0, m.w = p->w, m.h = p->h;
+  if (m.w == 0 && m.h == 0) m.x0 = 0, m.y0 = 0, m.w = m.W, m.h = m.H;
+  if (m.x0 < 0 || m.y0 < 0 || m.w < 0 || m.h < 0 || m.x0 + m.w > m.W || m.y0 + m.h > m.H) {
+    err = "tile outside the image";
+    return -1;
+  }
+  m.srows = 1, m.sidx = 0, m.scount = 1;
+  return (int64_t)m.w * m.h;
+}
+
+template <int STACK, bool FAST>
+int launch_intersect(rtx_scene* sc, const rtx_ray* d_rays, int64_t n, rtx_hit* d_hits, double tmin, double tmax,
+                     hipStream_t s) {
+  const int64_t blocks = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL((k_intersect<STACK, FAST>), dim3((unsigned)blocks), dim3(kBlock),
+                     STACK * kBlock * sizeof(uint32_t), s, sc->S, d_rays, n, d_hits, tmin, tmax);
+  HIPC(hipGetLastError());
+  return RTX_OK;
+}
+
+int persistent_grid(rtx_scene* sc, const void* fn, size_t lds) {
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kBlock, lds) != hipSuccess || per_cu <= 0)
+    per_cu = 1;
+  return std::max(1, per_cu) * sc->cus;
+}
+
+struct Launch {
+  rtx_scene* sc;
+  hipStream_t s;
+  int stack;
+  bool fast, count;
+};
+
+template <int STACK, bool FAST, bool COUNT>
+int run_extend(const Launch& L, const RenderArgs& A, const PathQueue& q, const unsigned* cnt, int64_t max_items) {
+  const size_t lds = STACK * kBlock * sizeof(uint32_t);
+  const int64_t need = (max_items + kBlock - 1) / kBlock;
+  const int grid = (int)std::max<int64_t>(
+      1, std::min<int64_t>(need, persistent_grid(L.sc, (const void*)k_wf_extend<STACK, FAST, COUNT>, lds)));
+  hipLaunchKernelGGL((k_wf_extend<STACK, FAST, COUNT>), dim3(grid), dim3(kBlock), lds, L.s, A, q, cnt);
+  HIPC(hipGetLastError());
+  return RTX_OK;
+}
+
+template <int STACK, bool FAST, bool COUNT, bool SCATTER>
+int run_persistent(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
+  const size_t lds = STACK * kBlock * sizeof(uint32_t);
+  const int grid = persistent_grid(L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER>, lds);
+  hipLaunchKernelGGL((k_persistent<STACK, FAST, COUNT, SCATTER>), dim3(grid), dim3(kBlock), lds, L.s, A, next_slot);
+  HIPC(hipGetLastError());
+  return RTX_OK;
+}
+
+// template dispatch helpers
+template <bool FAST, bool COUNT>
+int extend_s(const Launch& L, const RenderArgs& A, const PathQueue& q, const unsigned* c, int64_t n) {
+  return L.stack == 32 ? run_extend<32, FAST, COUNT>(L, A, q, c, n) : run_extend<64, FAST, COUNT>(L, A, q, c, n);
+}
+int extend(const Launch& L, const RenderArgs& A, const PathQueue& q, const unsigned* c, int64_t n) {
+  if (L.fast) return L.count ? extend_s<true, true>(L, A, q, c, n) : extend_s<true, false>(L, A, q, c, n);
+  return L.count ? extend_s<false, true>(L, A, q, c, n) : extend_s<false, false>(L, A, q, c, n);
+}
+template <bool FAST, bool COUNT, bool SCATTER>
+int persist_s(const Launch& L, const RenderArgs& A, unsigned long long* ns) {
+  return L.stack == 32 ? run_persistent<32, FAST, COUNT, SCATTER>(L, A, ns)
+                       : run_persistent<64, FAST, COUNT, SCATTER>(L, A, ns);
+}
+template <bool SCATTER>
+int persist_m(const Launch& L, const RenderArgs& A, unsigned long long* ns) {
+  if (L.fast) return L.count ? persist_s<true, true, SCATTER>(L, A, ns) : persist_s<true, false, SCATTER>(L, A, ns);
+  return L.count ? persist_s<false, true, SCATTER>(L, A, ns) : persist_s<false, false, SCATTER>(L, A, ns);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rtx_abi_version(void) { return RTX_ABI_VERSION; }
+const char* rtx_last_error(void) { return g_err.c_str(); }
+void rtx_internal_set_error(const char* msg) { g_err = msg ? msg : ""; }
+
+int rtx_device_count(int* n) {
+  if (!n) return fail(RTX_ERR_INVALID, "n is NULL");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess) {
+    *n = 0;
+    return fail(RTX_ERR_NODEVICE, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  }
+  *n = c;
+  return RTX_OK;
+}
+
+int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
+  if (!d || !out) return fail(RTX_ERR_INVALID, "NULL argument");
+  *out = nullptr;
+  if (d->n_prims < 0 || d->n_nodes < 0 || d->n_materials < 0 || d->n_textures < 0 || d->n_images < 0)
+    return fail(RTX_ERR_INVALID, "negative counts");
+  if (d->n_prims > 0 && !d->prims) return fail(RTX_ERR_INVALID, "prims is NULL");
+  // validate indices so kernels never read out of bounds
+  for (int64_t i = 0; i < d->n_prims; i++) {
+    const rtx_prim& p = d->prims[i];
+    if (p.kind < RTX_PRIM_SPHERE || p.kind > RTX_PRIM_YZ_RECT) return fail(RTX_ERR_INVALID, "bad primitive kind");
+    if (p.material < 0 || p.material >= d->n_materials) return fail(RTX_ERR_INVALID, "primitive material out of range");
+  }
+  for (int32_t i = 0; i < d->n_materials; i++) {
+    const rtx_material& m = d->materials[i];
+    if (m.kind < 0 || m.kind > RTX_MAT_DIFFUSE_LIGHT) return fail(RTX_ERR_INVALID, "bad material kind");
+    if ((m.kind == RTX_MAT_LAMBERTIAN || m.kind == RTX_MAT_DIFFUSE_LIGHT) && (m.texture < 0 || m.texture >= d->n_textures))
+      return fail(RTX_ERR_INVALID, "material texture out of range");
+  }
+  for (int32_t i = 0; i < d->n_textures; i++) {
+    const rtx_texture& t = d->textures[i];
+    if (t.kind == RTX_TEX_CHECKER && (t.even < 0 || t.even >= d->n_textures || t.odd < 0 || t.odd >= d->n_textures))
+      return fail(RTX_ERR_INVALID, "checker child out of range");
+    if (t.kind == RTX_TEX_IMAGE && t.image >= d->n_images) return fail(RTX_ERR_INVALID, "image index out of range");
+  }
+  for (int64_t i = 0; i < d->n_nodes; i++) {
+    const rtx_bvh_node& n = d->nodes[i];
+    if (n.is_leaf) {
+      if ((int64_t)n.left_first + n.right_count > d->n_prims) return fail(RTX_ERR_INVALID, "leaf range out of bounds");
+    } else if (n.left_first >= d->n_nodes || n.right_count >= d->n_nodes || n.left_first <= i || n.right_count <= i) {
+      return fail(RTX_ERR_INVALID, "child index out of bounds (nodes must be pre-order)");
+    }
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RTX_ERR_NODEVICE, "no HIP device");
+  if (device < 0 || device >= ndev) return fail(RTX_ERR_INVALID, "device out of range");
+  auto sc = std::make_unique<rtx_scene>();
+  sc->device = device;
+  HIPC(hipSetDevice(device));
+  hipDeviceProp_t prop;
+  HIPC(hipGetDeviceProperties(&prop, device));
+  sc->cus = prop.multiProcessorCount;
+  HIPC(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
+  for (auto& e : sc->ev) HIPC(hipEventCreate(&e));
+  hipStream_t s = sc->stream;
+  int rc;
+  if ((rc = upload(sc->prims, d->prims, d->n_prims, s))) return rc;
+  if ((rc = upload(sc->mats, d->materials, d->n_materials, s))) return rc;
+  if ((rc = upload(sc->texs, d->textures, d->n_textures, s))) return rc;
+  std::vector<DImage> imgs(d->n_images);
+  sc->texels.resize(d->n_images);
+  for (int32_t i = 0; i < d->n_images; i++) {
+    const rtx_image& im = d->images[i];
+    imgs[i].w = im.width, imgs[i].h = im.height, imgs[i].texels = nullptr;
+    if (im.width > 0 && im.height > 0 && im.texels) {
+      if ((rc = upload(sc->texels[i], im.texels, (size_t)im.width * im.height * 3, s))) return rc;
+      imgs[i].texels = sc->texels[i].as<uint8_t>();
+    } else {
+      imgs[i].w = imgs[i].h = 0;
+    }
+  }
+  if ((rc = upload(sc->images, imgs.data(), imgs.size(), s))) return rc;
+  sc->n_nodes = d->nodes ? d->n_nodes : 0;
+  std::vector<FNode> fn;
+  if (d->nodes && d->n_nodes > 0) {
+    if ((rc = upload(sc->nodes, d->nodes, d->n_nodes, s))) return rc;
+    const int depth = bvh_depth(d->nodes, d->n_nodes);
+    sc->stack_parity = pick_stack(depth);
+    sc->stack_fast = sc->stack_parity;
+    if (sc->stack_parity < 0) return fail(RTX_ERR_INVALID, "BVH deeper than 62 levels");
+    build_fast(d->nodes, d->n_nodes, fn);
+    if ((rc = upload(sc->fnodes, fn.data(), fn.size(), s))) return rc;
+  }
+  HIPC(hipStreamSynchronize(s));
+  DScene& S = sc->S;
+  S.nodes = sc->nodes.as<rtx_bvh_node>();
+  S.prims = sc->prims.as<rtx_prim>();
+  S.mats = sc->mats.as<rtx_material>();
+  S.texs = sc->texs.as<rtx_texture>();
+  S.images = sc->images.as<DImage>();
+  S.fnodes = fn.empty() ? nullptr : sc->fnodes.as<FNode>();
+  S.use_bvh = (d->nodes && d->n_nodes > 0) ? 1 : 0;
+  S.n_prims = S.use_bvh ? d->n_prims : d->n_prims;
+  S.froot_leaf = 0, S.froot_count = 0;
+  if (S.use_bvh && d->nodes[0].is_leaf) S.froot_leaf = 1, S.froot_count = (int32_t)d->nodes[0].right_count;
+  if (!d->nodes && d->n_nodes == 0) S.use_bvh = 0;
+  *out = sc.release();
+  return RTX_OK;
+}
+
+int rtx_scene_destroy(rtx_scene* s) {
+  delete s;
+  return RTX_OK;
+}
+
+int rtx_intersect_device(rtx_scene* sc, const rtx_ray* d_rays, size_t n, rtx_hit* d_hits, double tmin, double tmax,
+                         int32_t precision, void* stream) {
+  if (!sc) return fail(RTX_ERR_INVALID, "scene is NULL");
+  if (n == 0) return RTX_OK;
+  if (!d_rays || !d_hits) return fail(RTX_ERR_INVALID, "NULL buffer");
+  HIPC(hipSetDevice(sc->device));
+  hipStream_t s = stream ? (hipStream_t)stream : sc->stream;
+  const bool fast = precision == RTX_PREC_FAST && sc->S.fnodes;
+  const int st = fast ? sc->stack_fast : sc->stack_parity;
+  if (fast) return st == 32 ? launch_intersect<32, true>(sc, d_rays, (int64_t)n, d_hits, tmin, tmax, s)
+                            : launch_intersect<64, true>(sc, d_rays, (int64_t)n, d_hits, tmin, tmax, s);
+  return st == 32 ? launch_intersect<32, false>(sc, d_rays, (int64_t)n, d_hits, tmin, tmax, s)
+                  : launch_intersect<64, false>(sc, d_rays, (int64_t)n, d_hits, tmin, tmax, s);
+}
+
+int rtx_intersect(rtx_scene* sc, const rtx_ray* rays, size_t n, rtx_hit* hits, double tmin, double tmax,
+                  int32_t precision) {
+  if (!sc) return fail(RTX_ERR_INVALID, "scene is NULL");
+  if (n == 0) return RTX_OK;
+  if (!rays || !hits) return fail(RTX_ERR_INVALID, "NULL buffer");
+  HIPC(hipSetDevice(sc->device));
+  int rc;
+  if ((rc = sc->rays.reserve(n * sizeof(rtx_ray)))) return rc;
+  if ((rc = sc->hits.reserve(n * sizeof(rtx_hit)))) return rc;
+  HIPC(hipMemcpyAsync(sc->rays.p, rays, n * sizeof(rtx_ray), hipMemcpyHostToDevice, sc->stream));
+  if ((rc = rtx_intersect_device(sc, sc->rays.as<rtx_ray>(), n, sc->hits.as<rtx_hit>(), tmin, tmax, precision,
+                                 sc->stream)))
+    return rc;
+  HIPC(hipMemcpyAsync(hits, sc->hits.p, n * sizeof(rtx_hit), hipMemcpyDeviceToHost, sc->stream));
+  HIPC(hipStreamSynchronize(sc->stream));
+  return RTX_OK;
+}
+
+// Camera::Initialize (camera.h:100-131), same operation order as the reference.
+int rtx_camera_init(const rtx_camera_config* c, rtx_camera* o) {
+  if (!c || !o) return fail(RTX_ERR_INVALID, "NULL argument");
+  if (c->image_width <= 0 || !(c->aspect_ratio > 0)) return fail(RTX_ERR_INVALID, "bad image width / aspect ratio");
+  const double kPiH = 3.14159265358979323846;
+  auto sub = [](const double* a, const double* b, double* r) { for (int i = 0; i < 3; i++) r[i] = a[i] - b[i]; };
+  auto scale = [](double t, const double* a, double* r) { for (int i = 0; i < 3; i++) r[i] = t * a[i]; };
+  auto norm = [&](const double* a, double* r) {
+    double l = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+    if (l == 0.0) { r[0] = r[1] = r[2] = 0; return; }
+    scale(1.0 / l, a, r);
+  };
+  auto cross = [](const double* u, const double* v, double* r) {
+    r[0] = u[1] * v[2] - u[2] * v[1];
+    r[1] = u[2] * v[0] - u[0] * v[2];
+    r[2] = u[0] * v[1] - u[1] * v[0];
+  };
+  std::memset(o, 0, sizeof *o);
+  int H = int(c->image_width / c->aspect_ratio);
+  H = H < 1 ? 1 : H;
+  o->image_width = c->image_width, o->image_height = H;
+  for (int i = 0; i < 3; i++) o->center[i] = c->lookfrom[i];
+  double theta = c->vfov * (kPiH / 180.0);
+  double h = std::tan(theta / 2);
+  double vh = 2 * h * c->focus_dist;
+  double vw = vh * (double(c->image_width) / H);
+  double t[3], vu[3], vv[3], negv[3];
+  sub(c->lookfrom, c->lookat, t);
+  norm(t, o->w);
+  cross(c->vup, o->w, t);
+  norm(t, o->u);
+  cross(o->w, o->u, o->v);
+  scale(vw, o->u, vu);
+  for (int i = 0; i < 3; i++) negv[i] = -o->v[i];
+  scale(vh, negv, vv);
+  scale(1.0 / (double)c->image_width, vu, o->pixel_delta_u);
+  scale(1.0 / (double)H, vv, o->pixel_delta_v);
+  double fw[3], hu[3], hv[3], ul[3], sdd[3], hd[3];
+  scale(c->focus_dist, o->w, fw);
+  scale(1.0 / 2.0, vu, hu);
+  scale(1.0 / 2.0, vv, hv);
+  for (int i = 0; i < 3; i++) ul[i] = ((o->center[i] - fw[i]) - hu[i]) - hv[i];
+  for (int i = 0; i < 3; i++) sdd[i] = o->pixel_delta_u[i] + o->pixel_delta_v[i];
+  scale(0.5, sdd, hd);
+  for (int i = 0; i < 3; i++) o->pixel00[i] = ul[i] + hd[i];
+  double rad = c->focus_dist * std::tan((c->defocus_angle / 2) * (kPiH / 180.0));
+  scale(rad, o->u, o->defocus_disk_u);
+  scale(rad, o->v, o->defocus_disk_v);
+  o->defocus_angle = c->defocus_angle;
+  return RTX_OK;
+}
+
+int64_t rtx_render_pixel_count(const rtx_camera* cam, const rtx_render_params* p) {
+  if (!cam || !p) return fail(RTX_ERR_INVALID, "NULL argument");
+  PixelMap m;
+  std::string err;
+  int64_t n = subset_pixels(cam, p, m, err);
+  if (n < 0) return fail(RTX_ERR_INVALID, err);
+  return n;
+}
+
+int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm, double* d_rgb,
+                      int32_t* d_spp, rtx_stats* stats, void* stream) {
+  if (!sc || !cam || !prm || !d_rgb) return fail(RTX_ERR_INVALID, "NULL argument");
+  if (prm->spp < 0 || prm->max_depth < 0) return fail(RTX_ERR_INVALID, "negative spp / max_depth");
+  if (prm->mode < RTX_MODE_WAVEFRONT || prm->mode > RTX_MODE_MEGAKERNEL) return fail(RTX_ERR_INVALID, "bad mode");
+  if (prm->adaptive && prm->mode == RTX_MODE_MEGAKERNEL)
+    return fail(RTX_ERR_INVALID, "adaptive sampling is a WavefrontRenderer feature (use AdaptiveSampler semantics: not provided)");
+  PixelMap map;
+  std::string err;
+  const int64_t npix = subset_pixels(cam, prm, map, err);
+  if (npix < 0) return fail(RTX_ERR_INVALID, err);
+  HIPC(hipSetDevice(sc->device));
+  hipStream_t s = stream ? (hipStream_t)stream : sc->stream;
+  const bool fast = prm->precision == RTX_PREC_FAST && sc->S.fnodes;
+  Launch L{sc, s, fast ? sc->stack_fast : sc->stack_parity, fast, (prm->flags & RTX_FLAG_COUNT) != 0};
+
+  // samples in flight per pixel (group size K)
+  int K = prm->samples_per_group;
+  if (K <= 0) {
+    const int64_t target = 1ll << 25;
+    K = (int)std::max<int64_t>(1, std::min<int64_t>(prm->spp > 0 ? prm->spp : 1, target / std::max<int64_t>(1, npix)));
+  }
+  K = std::max(1, std::min(K, std::max(1, prm->spp)));
+  if ((int64_t)npix * K > 0xFFFFFFFFll) return fail(RTX_ERR_INVALID, "too many slots in one group (lower samples_per_group)");
+  const int64_t nslots = npix * (int64_t)K;
+
+  int rc;
+  if ((rc = sc->px_sum.reserve(npix * 3 * sizeof(double)))) return rc;
+  if ((rc = sc->px_mean.reserve(npix * 3 * sizeof(double)))) return rc;
+  if ((rc = sc->px_m2.reserve(npix * 3 * sizeof(double)))) return rc;
+  if ((rc = sc->px_samples.reserve(npix * sizeof(int32_t)))) return rc;
+  if ((rc = sc->px_conv.reserve(npix))) return rc;
+  if ((rc = sc->lbuf.reserve(nslots * 3 * sizeof(double)))) return rc;
+  if ((rc = sc->counters.reserve(64 * sizeof(unsigned long long)))) return rc;
+  const size_t qbytes = nslots * (9 * sizeof(double) + 3 * sizeof(uint32_t));
+  if (prm->mode == RTX_MODE_WAVEFRONT)
+    for (auto& q : sc->queue)
+      if ((rc = q.reserve(qbytes))) return rc;
+  HIPC(hipMemsetAsync(sc->px_sum.p, 0, npix * 3 * sizeof(double), s));
+  HIPC(hipMemsetAsync(sc->px_mean.p, 0, npix * 3 * sizeof(double), s));
+  HIPC(hipMemsetAsync(sc->px_m2.p, 0, npix * 3 * sizeof(double), s));
+  HIPC(hipMemsetAsync(sc->px_samples.p, 0, npix * sizeof(int32_t), s));
+  HIPC(hipMemsetAsync(sc->px_conv.p, 0, npix, s));
+  HIPC(hipMemsetAsync(sc->counters.p, 0, 64 * sizeof(unsigned long long), s));
+
+  unsigned long long* cnt = sc->counters.as<unsigned long long>();
+  PixelSoA px{sc->px_sum.as<double>(), sc->px_mean.as<double>(), sc->px_m2.as<double>(), sc->px_samples.as<int32_t>(),
+              sc->px_conv.as<uint8_t>()};
+  RenderArgs A;
+  A.S = sc->S;
+  A.cam = *cam;
+  A.map = map;
+  A.seed = prm->seed;
+  A.npix = npix;
+  A.max_depth = prm->max_depth;
+  A.scatter_api = prm->mode == RTX_MODE_MEGAKERNEL;
+  A.conv = prm->adaptive ? sc->px_conv.as<uint8_t>() : nullptr;
+  A.L = sc->lbuf.as<double>();
+  A.counters = cnt;
+  // counters[8..] : queue counts (u32) for the wavefront, [16] slot counter (persistent)
+  unsigned* qcount = (unsigned*)(cnt + 8);
+  unsigned long long* next_slot = cnt + 16;
+  auto make_queue = [&](DevBuf& b) {
+    PathQueue q;
+    double* d = b.as<double>();
+    q.ox = d, q.oy = d + nslots, q.oz = d + 2 * nslots, q.dx = d + 3 * nslots, q.dy = d + 4 * nslots;
+    q.dz = d + 5 * nslots, q.tx = d + 6 * nslots, q.ty = d + 7 * nslots, q.tz = d + 8 * nslots;
+    q.slot = (uint32_t*)(d + 9 * nslots);
+    q.meta = q.slot + nslots;
+    q.hit = (int32_t*)(q.meta + nslots);
+    return q;
+  };
+  // per-launch timing of the dominant kernel (extend / persistent) with an event pool
+  size_t evi = 0;
+  auto ev_at = [&](size_t i) -> hipEvent_t {
+    while (sc->evpool.size() <= i) {
+      hipEvent_t e = nullptr;
+      if (hipEventCreate(&e) != hipSuccess) return nullptr;
+      sc->evpool.push_back(e);
+    }
+    return sc->evpool[i];
+  };
+  const bool timed = stats != nullptr;
+  double hot_ms = 0;
+  uint64_t hot_launches = 0;
+  if (timed) HIPC(hipEventRecord(sc->ev[0], s));
+  const int pix_blocks = (int)((npix + kBlock - 1) / kBlock);
+  const int wf_grid = std::max(1, std::min<int>(sc->cus * 16, (int)((nslots + kBlock - 1) / kBlock)));
+  for (int s0 = 0, Kc = 0; s0 < prm->spp; s0 += Kc) {
+    Kc = std::min(K, prm->spp - s0);
+    // adaptive with automatic grouping: nothing can converge before min_spp, afterwards
+    // small groups limit the samples traced past a pixel's convergence point
+    if (prm->adaptive && prm->samples_per_group <= 0)
+      Kc = std::min(Kc, s0 < prm->min_spp ? prm->min_spp - s0 : 4);
+    A.K = Kc;
+    A.s0 = s0;
+    evi = 0;
+    auto hot_begin = [&]() -> int {
+      if (timed) {
+        hipEvent_t e = ev_at(evi++);
+        if (!e) return fail(RTX_ERR_HIP, "hipEventCreate failed");
+        HIPC(hipEventRecord(e, s));
+      }
+      return RTX_OK;
+    };
+    if (prm->mode == RTX_MODE_WAVEFRONT) {
+      PathQueue q[2] = {make_queue(sc->queue[0]), make_queue(sc->queue[1])};
+      HIPC(hipMemsetAsync(qcount, 0, 2 * sizeof(unsigned), s));
+      hipLaunchKernelGGL(k_wf_generate, dim3(wf_grid), dim3(kBlock), 0, s, A, q[0], qcount);
+      HIPC(hipGetLastError());
+      for (int b = 0; b <= prm->max_depth; b++) {
+        const int cur = b & 1;
+        HIPC(hipMemsetAsync(qcount + (cur ^ 1), 0, sizeof(unsigned), s));
+        if ((rc = hot_begin())) return rc;
+        if ((rc = extend(L, A, q[cur], qcount + cur, Kc * npix))) return rc;
+        if ((rc = hot_begin())) return rc;
+        hipLaunchKernelGGL(k_wf_shade, dim3(wf_grid), dim3(kBlock), 0, s, A, q[cur], qcount + cur, q[cur ^ 1],
+                           qcount + (cur ^ 1));
+        HIPC(hipGetLastError());
+        hot_launches++;
+      }
+    } else {
+      HIPC(hipMemsetAsync(next_slot, 0, sizeof(unsigned long long), s));
+      if ((rc = hot_begin())) return rc;
+      rc = prm->mode == RTX_MODE_MEGAKERNEL ? persist_m<true>(L, A, next_slot) : persist_m<false>(L, A, next_slot);
+      if (rc) return rc;
+      if ((rc = hot_begin())) return rc;
+      hot_launches++;
+    }
+    if (timed) {
+      HIPC(hipEventSynchronize(sc->evpool[evi - 1]));
+      for (size_t e = 0; e + 1 < evi; e += 2) {
+        float ms = 0;
+        HIPC(hipEventElapsedTime(&ms, sc->evpool[e], sc->evpool[e + 1]));
+        hot_ms += ms;
+      }
+    }
+    if (prm->mode == RTX_MODE_MEGAKERNEL)
+      hipLaunchKernelGGL(k_accumulate_sum, dim3(pix_blocks), dim3(kBlock), 0, s, px, A.L, npix, Kc);
+    else
+      hipLaunchKernelGGL(k_accumulate, dim3(pix_blocks), dim3(kBlock), 0, s, px, A.L, npix, Kc, prm->adaptive,
+                         prm->min_spp, prm->rel_threshold);
+    HIPC(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_resolve, dim3(pix_blocks), dim3(kBlock), 0, s, px, npix, prm->mode == RTX_MODE_MEGAKERNEL,
+                     prm->spp, d_rgb, d_spp);
+  HIPC(hipGetLastError());
+  if (timed) {
+    HIPC(hipEventRecord(sc->ev[1], s));
+    HIPC(hipEventSynchronize(sc->ev[1]));
+    float ms = 0;
+    HIPC(hipEventElapsedTime(&ms, sc->ev[0], sc->ev[1]));
+    unsigned long long h[4];
+    HIPC(hipMemcpy(h, cnt, sizeof h, hipMemcpyDeviceToHost));
+    stats->rays_total = h[0];
+    stats->rays_primary = h[1];
+    stats->paths = h[1];
+    stats->kernel_ms = ms;
+    stats->hot_kernel_ms = hot_ms;
+    stats->hot_launches = hot_launches;
+    stats->node_visits = h[2];
+    stats->prim_tests = h[3];
+  }
+  return RTX_OK;
+}
+
+int rtx_render(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm, double* rgb, int32_t* spp,
+               rtx_stats* stats) {
+  if (!sc || !cam || !prm || !rgb) return fail(RTX_ERR_INVALID, "NULL argument");
+  PixelMap map;
+  std::string err;
+  const int64_t npix = subset_pixels(cam, prm, map, err);
+  if (npix < 0) return fail(RTX_ERR_INVALID, err);
+  HIPC(hipSetDevice(sc->device));
+  int rc;
+  if ((rc = sc->out_rgb.reserve(std::max<int64_t>(1, npix) * 3 * sizeof(double)))) return rc;
+  if ((rc = sc->out_spp.reserve(std::max<int64_t>(1, npix) * sizeof(int32_t)))) return rc;
+  if ((rc = rtx_render_device(sc, cam, prm, sc->out_rgb.as<double>(), sc->out_spp.as<int32_t>(), stats, sc->stream)))
+    return rc;
+  HIPC(hipMemcpyAsync(rgb, sc->out_rgb.p, npix * 3 * sizeof(double), hipMemcpyDeviceToHost, sc->stream));
+  if (spp) HIPC(hipMemcpyAsync(spp, sc->out_spp.p, npix * sizeof(int32_t), hipMemcpyDeviceToHost, sc->stream));
+  HIPC(hipStreamSynchronize(sc->stream));
+  return RTX_OK;
+}
+
+// write_color (core/color.h:10-33): sqrt gamma, clamp [0, 0.999], int(256 x).
+int rtx_write_ppm(const char* path, const double* rgb, int32_t w, int32_t h) {
+  if (!path || !rgb || w <= 0 || h <= 0) return fail(RTX_ERR_INVALID, "bad argument");
+  FILE* f = std::fopen(path, "w");
+  if (!f) return fail(RTX_ERR_IO, std::string("cannot write ") + path);
+  std::fprintf(f, "P3\n%d %d\n255\n", w, h);
+  for (int64_t i = 0; i < (int64_t)w * h; i++) {
+    int b[3];
+    for (int c = 0; c < 3; c++) {
+      double x = rgb[3 * i + c];
+      x = x > 0 ? std::sqrt(x) : 0;
+      x = x < 0.0 ? 0.0 : (x > 0.999 ? 0.999 : x);
+      b[c] = int(256 * x);
+    }
+    std::fprintf(f, "%d %d %d\n", b[0], b[1], b[2]);
+  }
+  std::fclose(f);
+  return RTX_OK;
+}
+
+}  // extern "C"

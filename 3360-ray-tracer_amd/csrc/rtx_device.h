@@ -1,0 +1,739 @@
+// rtx_device.h — device-side building blocks of the MI355X path tracer (gfx950, wave64).
+//
+// Every function restates a reference routine (file:line under the reference's src/) in
+// the same IEEE double operation order, with the reference's float islands.  This file is
+// compiled with -ffp-contract=off: no FMA contraction anywhere in the f64 path, so parity
+// mode reproduces the CPU restatement (oracle/rtx_oracle.cc) bit for bit except where the
+// device libm (ocml cos/sin/acos/atan2/pow) differs from glibc in the last ulp.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rtx.h"
+
+namespace rtxd {
+
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kInf = __builtin_inf();
+
+// ---------------------------------------------------------------------------------------
+// Vec3 (vec3.h:8-107): a/t == (1/t)*a, left-to-right sums.
+// ---------------------------------------------------------------------------------------
+struct V3 {
+  double x, y, z;
+};
+__device__ __forceinline__ V3 v3(double x, double y, double z) { return V3{x, y, z}; }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ V3 operator-(V3 a) { return {-a.x, -a.y, -a.z}; }
+__device__ __forceinline__ V3 operator*(V3 a, V3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
+__device__ __forceinline__ V3 operator*(double t, V3 a) { return {t * a.x, t * a.y, t * a.z}; }
+__device__ __forceinline__ V3 operator/(V3 a, double t) { return (1.0 / t) * a; }
+__device__ __forceinline__ double comp(V3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+__device__ __forceinline__ double dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+__device__ __forceinline__ double len2(V3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+__device__ __forceinline__ V3 cross(V3 u, V3 v) {
+  return {u.y * v.z - u.z * v.y, u.z * v.x - u.x * v.z, u.x * v.y - u.y * v.x};
+}
+__device__ __forceinline__ bool near_zero(V3 a) {  // vec3.h:50-55
+  return fabs(a.x) < 1e-8 && fabs(a.y) < 1e-8 && fabs(a.z) < 1e-8;
+}
+__device__ __forceinline__ V3 normalize(V3 v) {  // math_utils.h:93-97
+  double l = sqrt(len2(v));
+  if (l == 0.0) return {0, 0, 0};
+  return v / l;
+}
+__device__ __forceinline__ V3 reflect(V3 v, V3 n) { return v - (2.0 * dot(v, n)) * n; }  // :14-16
+__device__ __forceinline__ V3 refract(V3 uv, V3 n, double eta) {                           // :24-29
+  double c = fmin(dot(-uv, n), 1.0);
+  V3 perp = eta * (uv + c * n);
+  V3 par = (-sqrt(fabs(1.0 - len2(perp)))) * n;
+  return perp + par;
+}
+
+// ---------------------------------------------------------------------------------------
+// Counter-based RNG: Philox-4x32-10, key (seed), counter (draw>>1, sample, pixel, 0).
+// Bit-identical to oracle/rtx_oracle.cc Rng::next (philox mode).  A path's stream depends
+// only on (seed, global pixel, sample), so results are independent of tiling, GPU count,
+// queue order and scheduling.
+// ---------------------------------------------------------------------------------------
+struct Rng {
+  uint32_t k0, k1, pixel, sample, draw;
+  __device__ __forceinline__ double next() {
+    uint32_t c0 = draw >> 1, c1 = sample, c2 = pixel, c3 = 0u;
+    uint32_t a = k0, b = k1;
+#pragma unroll
+    for (int r = 0; r < 10; r++) {
+      uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+      uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+      uint32_t n0 = hi1 ^ c1 ^ a;
+      uint32_t n2 = hi0 ^ c3 ^ b;
+      c0 = n0, c1 = lo1, c2 = n2, c3 = lo0;
+      a += 0x9E3779B9u;
+      b += 0xBB67AE85u;
+    }
+    uint32_t lo = (draw & 1) ? c2 : c0;
+    uint32_t hi = (draw & 1) ? c3 : c1;
+    draw++;
+    uint64_t bits = ((uint64_t)hi << 32) | lo;
+    return (double)(bits >> 11) * 0x1p-53;
+  }
+  __device__ __forceinline__ double next(double mn, double mx) { return mn + (mx - mn) * next(); }
+};
+__device__ __forceinline__ Rng make_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t draw) {
+  Rng g;
+  g.k0 = (uint32_t)seed;
+  g.k1 = (uint32_t)(seed >> 32) ^ 0x52545831u;
+  g.pixel = pixel, g.sample = sample, g.draw = draw;
+  return g;
+}
+
+// RandomUnitVector (math_utils.h:62-70): draws z, y, x (g++ right-to-left argument order).
+__device__ __forceinline__ V3 random_unit_vector(Rng& g) {
+  while (true) {
+    double z = g.next(-1.0, 1.0);
+    double y = g.next(-1.0, 1.0);
+    double x = g.next(-1.0, 1.0);
+    V3 p{x, y, z};
+    double l2 = len2(p);
+    if (l2 > 1e-12 && l2 <= 1.0) return p / sqrt(l2);
+  }
+}
+__device__ __forceinline__ V3 random_in_unit_disk(Rng& g) {  // math_utils.h:83-88
+  while (true) {
+    double y = g.next(-1, 1);
+    double x = g.next(-1, 1);
+    V3 p{x, y, 0.0};
+    if (len2(p) < 1.0) return p;
+  }
+}
+__device__ __forceinline__ V3 random_cosine_direction(Rng& g, V3 normal) {  // math_utils.h:104-123
+  double r1 = g.next();
+  double r2 = g.next();
+  double phi = 2.0 * kPi * r1;
+  double r = sqrt(r2);
+  double x = r * cos(phi);
+  double y = r * sin(phi);
+  double z = sqrt(1.0 - r2);
+  V3 w = normalize(normal);
+  V3 a = (fabs(w.x) > 0.9) ? v3(0, 1, 0) : v3(1, 0, 0);
+  V3 v = normalize(cross(w, a));
+  V3 u = cross(v, w);
+  return normalize(x * u + y * v + z * w);
+}
+
+// ---------------------------------------------------------------------------------------
+// Device scene (uploaded once per device by rtx_scene_create)
+// ---------------------------------------------------------------------------------------
+struct DImage {
+  int32_t w, h;
+  const uint8_t* texels;
+};
+
+// Fast-path BVH2 node (RTX_PREC_FAST): both children's f32 boxes in the parent, so one
+// 64-byte line decides the near/far order.  Boxes are the f64 boxes rounded outward and
+// padded by the scene's conservative epsilon (see csrc/rtx_capi.hip build_fast_bvh).
+// child >= 0: internal node index; child < 0: leaf, ~child = first prim, count in cnt.
+struct FNode {
+  float lo0[3], hi0[3];
+  float lo1[3], hi1[3];
+  int32_t c0, c1;
+  uint16_t n0, n1;  // leaf primitive counts (0 for internal children)
+  uint32_t pad_;
+};
+static_assert(sizeof(FNode) == 64, "FNode must be one 64-byte line");
+
+struct DScene {
+  const rtx_bvh_node* nodes;  // parity layout, reference pre-order
+  const rtx_prim* prims;      // leaf order
+  const rtx_material* mats;
+  const rtx_texture* texs;
+  const DImage* images;
+  const FNode* fnodes;  // fast layout (root at 0) or nullptr
+  int64_t n_prims;
+  int32_t use_bvh;
+  int32_t froot_leaf;  // fast BVH: the whole tree is one leaf (count in froot_count)
+  int32_t froot_count;
+  int32_t pad_;
+};
+
+struct Hit {  // HitRecord (hittable.h:18-42)
+  V3 p, normal;
+  double t, u, v;
+  int32_t mat;
+  int32_t front_face;
+  // Sphere u,v (acos/atan2, sphere.h:73-79) are only ever read by image textures, so the
+  // shading path defers them: lazy_sphere >= 0 names the sphere whose u,v are still to be
+  // derived from p (same arithmetic as at hit time, hence the same values).
+  int64_t lazy_sphere;
+};
+
+__device__ __forceinline__ void set_face_normal(Hit& h, V3 d, V3 outward) {  // hittable.h:31-34
+  h.front_face = dot(d, outward) < 0;
+  h.normal = h.front_face ? outward : -outward;
+}
+
+__device__ __forceinline__ void sphere_uv(V3 outward, double& u, double& v) {  // get_sphere_uv
+  double theta = acos(-outward.y);
+  double phi = atan2(-outward.z, outward.x) + kPi;
+  u = phi / (2 * kPi);
+  v = theta / kPi;
+}
+
+// Sphere::Hit + get_sphere_uv (sphere.h:23-55,73-79)
+template <bool UV = true>
+__device__ __forceinline__ bool hit_sphere(const double* g, int32_t mat, V3 o, V3 d, double tmin, double tmax,
+                                           Hit& rec) {
+  V3 c{g[0], g[1], g[2]};
+  double radius = fmax(0.0, g[3]);
+  V3 oc = c - o;
+  double a = len2(d);
+  double h = dot(d, oc);
+  double cc = len2(oc) - radius * radius;
+  double disc = h * h - a * cc;
+  if (disc < 0) return false;
+  double sq = sqrt(disc);
+  double root = (h - sq) / a;
+  if (!(tmin < root && root < tmax)) {
+    root = (h + sq) / a;
+    if (!(tmin < root && root < tmax)) return false;
+  }
+  rec.t = root;
+  rec.p = o + rec.t * d;
+  V3 outward = (rec.p - c) / radius;
+  set_face_normal(rec, d, outward);
+  if (UV) sphere_uv(outward, rec.u, rec.v);
+  rec.mat = mat;
+  return true;
+}
+
+// Triangle::Hit (triangle.h:41-87): f32 det/inv_det/u/v/t, inclusive range, u,v untouched.
+__device__ __forceinline__ bool hit_triangle(const double* g, int32_t mat, V3 o, V3 d, double tmin, double tmax,
+                                             Hit& rec) {
+  V3 A{g[0], g[1], g[2]}, B{g[3], g[4], g[5]}, C{g[6], g[7], g[8]};
+  V3 e1 = B - A, e2 = C - A;
+  V3 pvec = cross(d, e2);
+  float det = (float)dot(e1, pvec);
+  if (fabsf(det) < 1e-6f) return false;
+  float inv_det = 1.0f / det;
+  V3 tvec = o - A;
+  float u = (float)(dot(tvec, pvec) * (double)inv_det);
+  if (u < 0.0f || u > 1.0f) return false;
+  V3 qvec = cross(tvec, e1);
+  float v = (float)(dot(d, qvec) * (double)inv_det);
+  if (v < 0.0f || (u + v) > 1.0f) return false;
+  float t = (float)(dot(e2, qvec) * (double)inv_det);
+  if ((double)t < tmin || (double)t > tmax) return false;
+  rec.t = (double)t;
+  rec.p = o + rec.t * d;
+  rec.mat = mat;
+  set_face_normal(rec, d, normalize(cross(e1, e2)));
+  return true;
+}
+
+// xy/xz/yz_rect::Hit (rect.h:19-40, 65-85, 109-130)
+__device__ __forceinline__ bool hit_rect(int kind, const double* g, int32_t mat, V3 o, V3 d, double tmin,
+                                         double tmax, Hit& rec) {
+  int ax, a0, a1;
+  V3 n;
+  if (kind == RTX_PRIM_XY_RECT) ax = 2, a0 = 0, a1 = 1, n = v3(0, 0, 1);
+  else if (kind == RTX_PRIM_XZ_RECT) ax = 1, a0 = 0, a1 = 2, n = v3(0, 1, 0);
+  else ax = 0, a0 = 1, a1 = 2, n = v3(1, 0, 0);
+  double t = (g[4] - comp(o, ax)) / comp(d, ax);
+  if (!(tmin < t && t < tmax)) return false;
+  double x = comp(o, a0) + t * comp(d, a0);
+  double y = comp(o, a1) + t * comp(d, a1);
+  if (x < g[0] || x > g[1] || y < g[2] || y > g[3]) return false;
+  rec.u = (x - g[0]) / (g[1] - g[0]);
+  rec.v = (y - g[2]) / (g[3] - g[2]);
+  rec.t = t;
+  set_face_normal(rec, d, n);
+  rec.mat = mat;
+  rec.p = o + rec.t * d;
+  return true;
+}
+
+template <bool UV = true>
+__device__ __forceinline__ bool hit_prim(const rtx_prim* __restrict__ P, V3 o, V3 d, double tmin, double tmax,
+                                         Hit& rec) {
+  const int kind = P->kind;
+  const int32_t mat = P->material;
+  double g[9];
+  if (kind == RTX_PRIM_TRIANGLE) {
+#pragma unroll
+    for (int i = 0; i < 9; i++) g[i] = P->g[i];
+    return hit_triangle(g, mat, o, d, tmin, tmax, rec);
+  }
+  if (kind == RTX_PRIM_SPHERE) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) g[i] = P->g[i];
+    return hit_sphere<UV>(g, mat, o, d, tmin, tmax, rec);
+  }
+#pragma unroll
+  for (int i = 0; i < 5; i++) g[i] = P->g[i];
+  return hit_rect(kind, g, mat, o, d, tmin, tmax, rec);
+}
+
+// Accept/reject + distance only: the same arithmetic and decisions as hit_sphere /
+// hit_triangle / hit_rect up to the point where they accept, without building the record.
+// Traversal keeps just (closest t, best primitive); finish_hit() rebuilds the record of the
+// winner afterwards with the interval (tmin, +inf), which yields the same root/t and hence
+// the identical record (sphere: the near root is re-selected iff it was accepted).
+__device__ __forceinline__ bool prim_t(const rtx_prim* __restrict__ P, V3 o, V3 d, double tmin, double tmax,
+                                       double& t_out) {
+  const int kind = P->kind;
+  if (kind == RTX_PRIM_TRIANGLE) {
+    V3 A{P->g[0], P->g[1], P->g[2]}, B{P->g[3], P->g[4], P->g[5]}, C{P->g[6], P->g[7], P->g[8]};
+    V3 e1 = B - A, e2 = C - A;
+    V3 pvec = cross(d, e2);
+    float det = (float)dot(e1, pvec);
+    if (fabsf(det) < 1e-6f) return false;
+    float inv_det = 1.0f / det;
+    V3 tvec = o - A;
+    float u = (float)(dot(tvec, pvec) * (double)inv_det);
+    if (u < 0.0f || u > 1.0f) return false;
+    V3 qvec = cross(tvec, e1);
+    float v = (float)(dot(d, qvec) * (double)inv_det);
+    if (v < 0.0f || (u + v) > 1.0f) return false;
+    float t = (float)(dot(e2, qvec) * (double)inv_det);
+    if ((double)t < tmin || (double)t > tmax) return false;
+    t_out = (double)t;
+    return true;
+  }
+  if (kind == RTX_PRIM_SPHERE) {
+    V3 c{P->g[0], P->g[1], P->g[2]};
+    double radius = fmax(0.0, P->g[3]);
+    V3 oc = c - o;
+    double a = len2(d);
+    double h = dot(d, oc);
+    double cc = len2(oc) - radius * radius;
+    double disc = h * h - a * cc;
+    if (disc < 0) return false;
+    double sq = sqrt(disc);
+    double root = (h - sq) / a;
+    if (!(tmin < root && root < tmax)) {
+      root = (h + sq) / a;
+      if (!(tmin < root && root < tmax)) return false;
+    }
+    t_out = root;
+    return true;
+  }
+  int ax, a0, a1;
+  if (kind == RTX_PRIM_XY_RECT) ax = 2, a0 = 0, a1 = 1;
+  else if (kind == RTX_PRIM_XZ_RECT) ax = 1, a0 = 0, a1 = 2;
+  else ax = 0, a0 = 1, a1 = 2;
+  double t = (P->g[4] - comp(o, ax)) / comp(d, ax);
+  if (!(tmin < t && t < tmax)) return false;
+  double x = comp(o, a0) + t * comp(d, a0);
+  double y = comp(o, a1) + t * comp(d, a1);
+  if (x < P->g[0] || x > P->g[1] || y < P->g[2] || y > P->g[3]) return false;
+  t_out = t;
+  return true;
+}
+
+// Rebuild the HitRecord of the closest primitive (see prim_t).  u, v start at 0: the
+// reference leaves them stale for triangles (triangle.h:77-84).
+template <bool UV = true>
+__device__ __forceinline__ void finish_hit(const DScene& S, int64_t best, V3 o, V3 d, double tmin, Hit& h) {
+  h.u = 0.0, h.v = 0.0;
+  hit_prim<UV>(S.prims + best, o, d, tmin, kInf, h);
+  h.lazy_sphere = (!UV && S.prims[best].kind == RTX_PRIM_SPHERE) ? best : -1;
+}
+
+// Aabb::Hit (aabb.h:92-115), f64, relies on IEEE 1/0 = inf and false NaN compares.
+__device__ __forceinline__ bool box_hit(const double* lo, const double* hi, V3 o, V3 inv_unused, V3 d,
+                                        double tmin, double tmax) {
+#pragma unroll
+  for (int a = 0; a < 3; a++) {
+    const double adinv = 1.0 / comp(d, a);
+    double t0 = (lo[a] - comp(o, a)) * adinv;
+    double t1 = (hi[a] - comp(o, a)) * adinv;
+    if (t0 < t1) {
+      if (t0 > tmin) tmin = t0;
+      if (t1 < tmax) tmax = t1;
+    } else {
+      if (t1 > tmin) tmin = t1;
+      if (t0 < tmax) tmax = t0;
+    }
+    if (tmax <= tmin) return false;
+  }
+  return true;
+}
+
+struct Counters {
+  uint32_t nodes, prims;
+};
+
+// ---------------------------------------------------------------------------------------
+// Parity traversal: Scene{Bvh}::Hit exactly as bvh.h:71-119 (stack, push right then left,
+// f64 slab test on [tmin, closest]).  The stack lives in LDS, one column per lane:
+// stack entry i of lane t at stk[i * stride + t] (consecutive lanes -> consecutive banks).
+// ---------------------------------------------------------------------------------------
+// Returns the index (leaf order) of the closest primitive, or -1.
+template <int STACK, bool COUNT>
+__device__ __forceinline__ int64_t trace_parity(const DScene& S, V3 o, V3 d, double tmin, double tmax,
+                                                uint32_t* stk, int stride, Counters& cnt) {
+  int64_t best = -1;
+  double closest = tmax, t;
+  if (!S.use_bvh) {  // scene::Scene::Hit linear list (scene.h:47-61)
+    for (int64_t i = 0; i < S.n_prims; i++) {
+      if (COUNT) cnt.prims++;
+      if (prim_t(S.prims + i, o, d, tmin, closest, t)) closest = t, best = i;
+    }
+    return best;
+  }
+  int sp = 0;
+  stk[0] = 0u;
+  sp = 1;
+  while (sp > 0) {
+    const uint32_t ni = stk[(--sp) * stride];
+    const rtx_bvh_node* __restrict__ nd = S.nodes + ni;
+    double lo[3] = {nd->lo[0], nd->lo[1], nd->lo[2]};
+    double hi[3] = {nd->hi[0], nd->hi[1], nd->hi[2]};
+    const uint32_t a = nd->left_first, b = nd->right_count, leaf = nd->is_leaf;
+    if (COUNT) cnt.nodes++;
+    if (!box_hit(lo, hi, o, o, d, tmin, closest)) continue;
+    if (leaf) {
+      for (uint32_t i = 0; i < b; i++) {
+        if (COUNT) cnt.prims++;
+        if (prim_t(S.prims + a + i, o, d, tmin, closest, t)) closest = t, best = (int64_t)a + i;
+      }
+    } else {
+      if (sp + 2 > STACK) __builtin_trap();  // host sizes STACK >= tree depth + 1
+      stk[(sp++) * stride] = b;
+      stk[(sp++) * stride] = a;
+    }
+  }
+  return best;
+}
+
+// ---------------------------------------------------------------------------------------
+// Fast traversal (RTX_PREC_FAST): f32 slab tests against conservatively enlarged boxes,
+// nearer child first; leaves are tested with the exact f64 primitive routines above.
+// Enlarged boxes accept every ray the f64 test accepts, so the set of primitives that can
+// produce the closest hit is a superset of the reference's; the closest hit is the same
+// except for exact-tie orderings between distinct primitives (measure zero).
+// ---------------------------------------------------------------------------------------
+// The f64 origin is split into hi + lo floats so that (box - origin) is formed with a
+// RELATIVE rounding error (no absolute error from rounding |o| to f32); together with the
+// relative slack below and outward-rounded boxes the f32 test never rejects a box the
+// reference's f64 test accepts.
+struct FRay {
+  float ohx, ohy, ohz, olx, oly, olz, ix, iy, iz;
+};
+__device__ __forceinline__ FRay make_fray(V3 o, V3 d) {
+  FRay r;
+  r.ohx = (float)o.x, r.ohy = (float)o.y, r.ohz = (float)o.z;
+  r.olx = (float)(o.x - (double)r.ohx), r.oly = (float)(o.y - (double)r.ohy), r.olz = (float)(o.z - (double)r.ohz);
+  r.ix = 1.0f / (float)d.x, r.iy = 1.0f / (float)d.y, r.iz = 1.0f / (float)d.z;
+  return r;
+}
+// Returns the (slack-widened) entry distance, or +inf on a miss.
+__device__ __forceinline__ float fbox(const float* lo, const float* hi, const FRay& r, float tmin_f, float tmax_f) {
+  float tx0 = ((lo[0] - r.ohx) - r.olx) * r.ix, tx1 = ((hi[0] - r.ohx) - r.olx) * r.ix;
+  float ty0 = ((lo[1] - r.ohy) - r.oly) * r.iy, ty1 = ((hi[1] - r.ohy) - r.oly) * r.iy;
+  float tz0 = ((lo[2] - r.ohz) - r.olz) * r.iz, tz1 = ((hi[2] - r.ohz) - r.olz) * r.iz;
+  // fminf/fmaxf drop a NaN operand (0*inf for an axis-parallel ray on a slab plane); the
+  // reference rejects those rays, so dropping the constraint only widens the accepted set.
+  float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin_f));
+  float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax_f));
+  tn = tn * 0.99999f;  // relative slack >> the ~6 ulp of f32 rounding in the products
+  tf = tf * 1.00001f;
+  return tn <= tf ? tn : __builtin_inff();
+}
+
+// smallest float >= x (x > 0 or +inf here)
+__device__ __forceinline__ float f32_round_up(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = __int_as_float(__float_as_int(f) + (f >= 0.0f ? 1 : -1));
+  return f;
+}
+
+template <int STACK, bool COUNT>
+__device__ __forceinline__ int64_t trace_fast(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
+                                              int stride, Counters& cnt) {
+  int64_t best = -1;
+  double closest = tmax, t;
+  if (!S.use_bvh || S.froot_leaf) {
+    const int64_t n = S.use_bvh ? S.froot_count : S.n_prims;
+    for (int64_t i = 0; i < n; i++) {
+      if (COUNT) cnt.prims++;
+      if (prim_t(S.prims + i, o, d, tmin, closest, t)) closest = t, best = i;
+    }
+    return best;
+  }
+  const FRay r = make_fray(o, d);
+  const float tmin_f = 0.0f;  // boxes only need t >= 0 for conservativeness (tmin > 0)
+  float tmax_f = f32_round_up(closest);
+  int sp = 0;
+  int32_t node = 0;
+  while (true) {
+    const FNode* __restrict__ nd = S.fnodes + node;
+    float lo0[3] = {nd->lo0[0], nd->lo0[1], nd->lo0[2]}, hi0[3] = {nd->hi0[0], nd->hi0[1], nd->hi0[2]};
+    float lo1[3] = {nd->lo1[0], nd->lo1[1], nd->lo1[2]}, hi1[3] = {nd->hi1[0], nd->hi1[1], nd->hi1[2]};
+    int32_t c0 = nd->c0, c1 = nd->c1;
+    uint32_t n0 = nd->n0, n1 = nd->n1;
+    if (COUNT) cnt.nodes++;
+    float t0 = fbox(lo0, hi0, r, tmin_f, tmax_f);
+    float t1 = fbox(lo1, hi1, r, tmin_f, tmax_f);
+    bool h0 = t0 != __builtin_inff(), h1 = t1 != __builtin_inff();
+    // leaves are processed immediately, internal children are traversed near-first
+    bool shrink = false;
+    if (h0 && c0 < 0) {
+      uint32_t first = (uint32_t)(~c0);
+      for (uint32_t i = 0; i < n0; i++) {
+        if (COUNT) cnt.prims++;
+        if (prim_t(S.prims + first + i, o, d, tmin, closest, t)) closest = t, best = (int64_t)first + i, shrink = true;
+      }
+      h0 = false;
+    }
+    if (h1 && c1 < 0) {
+      uint32_t first = (uint32_t)(~c1);
+      for (uint32_t i = 0; i < n1; i++) {
+        if (COUNT) cnt.prims++;
+        if (prim_t(S.prims + first + i, o, d, tmin, closest, t)) closest = t, best = (int64_t)first + i, shrink = true;
+      }
+      h1 = false;
+    }
+    if (shrink) tmax_f = f32_round_up(closest);
+    if (h0 && h1) {
+      int32_t nearc = t0 <= t1 ? c0 : c1;
+      int32_t farc = t0 <= t1 ? c1 : c0;
+      if (sp + 1 > STACK) __builtin_trap();
+      stk[(sp++) * stride] = (uint32_t)farc;
+      node = nearc;
+    } else if (h0) {
+      node = c0;
+    } else if (h1) {
+      node = c1;
+    } else {
+      // pop, re-testing the popped node's box against the shrunk interval is implicit:
+      // its box was tested when pushed; a stale far child is re-culled at its own node.
+      if (sp == 0) break;
+      node = (int32_t)stk[(--sp) * stride];
+    }
+  }
+  return best;
+}
+
+// ---------------------------------------------------------------------------------------
+// Textures / materials
+// ---------------------------------------------------------------------------------------
+// Deferred get_sphere_uv for image textures: outward = (p - c) / r exactly as hit_sphere.
+__device__ __noinline__ void lazy_sphere_uv(const rtx_prim* __restrict__ P, V3 p, double& u, double& v) {
+  V3 c{P->g[0], P->g[1], P->g[2]};
+  double radius = fmax(0.0, P->g[3]);
+  sphere_uv((p - c) / radius, u, v);
+}
+
+__device__ __forceinline__ V3 tex_value(const DScene& S, int32_t t, const Hit& rec) {
+  double u = rec.u, v = rec.v;
+  const V3 p = rec.p;
+  for (int guard = 0; guard < 16; guard++) {
+    const rtx_texture T = S.texs[t];
+    if (T.kind == RTX_TEX_SOLID) return v3(T.color[0], T.color[1], T.color[2]);
+    if (T.kind == RTX_TEX_CHECKER) {  // texture.h:37-45 (C++ % keeps the sign)
+      int xi = (int)floor(T.inv_scale * p.x);
+      int yi = (int)floor(T.inv_scale * p.y);
+      int zi = (int)floor(T.inv_scale * p.z);
+      t = ((xi + yi + zi) % 2 == 0) ? T.even : T.odd;
+      continue;
+    }
+    // ImageTexture::Value (texture.h:58-73), Image::PixelData/Clamp (image.cc:50-67)
+    if (T.image < 0) return v3(0, 1, 1);
+    const DImage im = S.images[T.image];
+    if (im.h <= 0) return v3(0, 1, 1);
+    if (rec.lazy_sphere >= 0) lazy_sphere_uv(S.prims + rec.lazy_sphere, p, u, v);
+    u = u < 0 ? 0 : (u > 1 ? 1 : u);
+    v = 1.0 - (v < 0 ? 0 : (v > 1 ? 1 : v));
+    int i = (int)(u * im.w);
+    int j = (int)(v * im.h);
+    i = i < 0 ? 0 : (i < im.w ? i : im.w - 1);
+    j = j < 0 ? 0 : (j < im.h ? j : im.h - 1);
+    const uint8_t* px = im.texels + ((size_t)j * im.w + i) * 3;
+    double s = 1.0 / 255.0;
+    return v3(s * px[0], s * px[1], s * px[2]);
+  }
+  return v3(0, 1, 1);
+}
+
+// pow(x, 5.0) (material.cc:261) as a double-double product chain rounded once: the
+// correctly rounded x^5, which is what glibc's pow (<= 0.52 ulp) returns except at
+// near-ties.  Explicit fma() only builds the exact error terms (no contraction elsewhere).
+__device__ __forceinline__ double pow5(double x) {
+  const double p2 = x * x, e2 = fma(x, x, -p2);
+  const double p4 = p2 * p2, e4 = fma(p2, p2, -p4) + 2.0 * (p2 * e2);
+  const double p5 = p4 * x, e5 = fma(p4, x, -p5) + e4 * x;
+  return p5 + e5;
+}
+
+__device__ __forceinline__ double reflectance(double c, double ri) {  // material.cc:258-262
+  double r0 = (1.0 - ri) / (1.0 + ri);
+  r0 = r0 * r0;
+  return r0 + (1.0 - r0) * pow5(1.0 - c);
+}
+
+// Material::Sample (material.cc:57-74, 117-141, 194-256, 302-310)
+__device__ __forceinline__ bool mat_sample(const DScene& S, const rtx_material& m, const Hit& rec, V3 wo, V3& wi,
+                                           float& pdf, V3& f, Rng& g) {
+  if (m.kind == RTX_MAT_LAMBERTIAN) {
+    wi = random_cosine_direction(g, rec.normal);
+    if (dot(wi, rec.normal) <= 0) return false;
+    float c = (float)dot(rec.normal, wi);
+    pdf = (c <= 0.0f) ? 0.0f : (float)((double)c / kPi);
+    if (dot(rec.normal, wi) <= 0) f = v3(0, 0, 0);
+    else f = tex_value(S, m.texture, rec) / kPi;
+    return true;
+  }
+  if (m.kind == RTX_MAT_METAL) {
+    wi = reflect(-wo, rec.normal);
+    wi = wi + m.fuzz * random_unit_vector(g);
+    wi = normalize(wi);
+    if (dot(wi, rec.normal) <= 0) return false;
+    pdf = 1.0f;
+    f = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
+    return true;
+  }
+  if (m.kind == RTX_MAT_DIELECTRIC) {
+    V3 n = rec.normal;
+    double eta_i = 1.0, eta_t = m.ref_idx;
+    if (!rec.front_face) {
+      double tt = eta_i;
+      eta_i = eta_t, eta_t = tt;
+    }
+    double eta = eta_i / eta_t;
+    V3 win = -normalize(wo);
+    double ci = dot(win, n);
+    ci = ci < -1.0 ? -1.0 : (ci > 1.0 ? 1.0 : ci);
+    double si = sqrt(fmax(0.0, 1.0 - ci * ci));
+    double st = eta * si;
+    pdf = 1.0f;
+    if (st >= 1.0) {
+      wi = reflect(win, n);
+      f = v3(1.0, 1.0, 1.0);
+      return true;
+    }
+    double Fr = reflectance(fabs(ci), m.ref_idx);
+    if (g.next() < Fr) {
+      wi = reflect(win, n);
+      f = v3(1.0, 1.0, 1.0);
+      return true;
+    }
+    wi = refract(win, n, eta);
+    double k = eta * eta;
+    f = v3(k, k, k);
+    return true;
+  }
+  return false;  // DiffuseLight
+}
+
+// Material::Scatter (material.cc:20-34, 82-94, 148-172, 273-280) — megakernel mode
+__device__ __forceinline__ bool mat_scatter(const DScene& S, const rtx_material& m, V3 rin_d, const Hit& rec,
+                                            V3& att, V3& sd, Rng& g) {
+  if (m.kind == RTX_MAT_LAMBERTIAN) {
+    V3 dir = rec.normal + random_unit_vector(g);
+    if (near_zero(dir)) dir = rec.normal;
+    sd = dir;
+    att = tex_value(S, m.texture, rec);
+    return true;
+  }
+  if (m.kind == RTX_MAT_METAL) {
+    V3 r = reflect(rin_d, rec.normal);
+    r = r + m.fuzz * random_unit_vector(g);
+    sd = r;
+    att = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
+    return dot(sd, rec.normal) > 0;
+  }
+  if (m.kind == RTX_MAT_DIELECTRIC) {
+    att = v3(1.0, 1.0, 1.0);
+    double eta = rec.front_face ? (1.0 / m.ref_idx) : m.ref_idx;
+    V3 ud = normalize(rin_d);
+    double ct = fmin(dot(-ud, rec.normal), 1.0);
+    double stt = sqrt(1.0 - ct * ct);
+    bool cannot = eta * stt > 1.0;
+    if (cannot || reflectance(ct, eta) > g.next()) sd = reflect(ud, rec.normal);
+    else sd = refract(ud, rec.normal, eta);
+    return true;
+  }
+  return false;
+}
+
+__device__ __forceinline__ V3 mat_emitted(const DScene& S, const rtx_material& m, const Hit& rec) {
+  if (m.kind == RTX_MAT_DIFFUSE_LIGHT) return tex_value(S, m.texture, rec);
+  return v3(0, 0, 0);
+}
+
+__device__ __forceinline__ V3 sky(V3 d) {  // wavefront.cc:33-38, camera.h:171-173
+  V3 ud = normalize(d);
+  double t = 0.5 * (ud.y + 1.0);
+  return (1.0 - t) * v3(1.0, 1.0, 1.0) + t * v3(0.5, 0.7, 1.0);
+}
+
+// Camera::GetRay (camera.h:134-144,196-203): y offset drawn first (g++ arg order).
+__device__ __forceinline__ void get_ray(const rtx_camera& c, int i, int j, Rng& g, V3& o, V3& d) {
+  double oy = g.next() - 0.5;
+  double ox = g.next() - 0.5;
+  V3 p00{c.pixel00[0], c.pixel00[1], c.pixel00[2]};
+  V3 du{c.pixel_delta_u[0], c.pixel_delta_u[1], c.pixel_delta_u[2]};
+  V3 dv{c.pixel_delta_v[0], c.pixel_delta_v[1], c.pixel_delta_v[2]};
+  V3 ps = p00 + ((i + ox) * du) + ((j + oy) * dv);
+  V3 center{c.center[0], c.center[1], c.center[2]};
+  if (c.defocus_angle <= 0) {
+    o = center;
+  } else {
+    V3 p = random_in_unit_disk(g);
+    V3 ddu{c.defocus_disk_u[0], c.defocus_disk_u[1], c.defocus_disk_u[2]};
+    V3 ddv{c.defocus_disk_v[0], c.defocus_disk_v[1], c.defocus_disk_v[2]};
+    o = center + (p.x * ddu) + (p.y * ddv);
+  }
+  d = ps - o;
+}
+
+// Path state between bounces (RayState, ray_state.h:8-13) + RNG draw counter.
+struct Path {
+  V3 o, d, thr;
+  int32_t depth;
+  uint32_t draw;
+};
+
+// One shading step (wavefront.cc:109-208).  true: continue with p updated; false: path
+// terminated with radiance L (RecordSample is done by the caller, in sample order).
+__device__ __forceinline__ bool shade(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit, Rng& g,
+                                      V3& L) {
+  L = v3(0, 0, 0);
+  if (!hit || p.depth >= max_depth) {
+    L = L + p.thr * sky(p.d);
+    return false;
+  }
+  const rtx_material m = S.mats[rec.mat];
+  V3 em = mat_emitted(S, m, rec);
+  if (!near_zero(em)) {
+    L = L + p.thr * em;
+    return false;
+  }
+  V3 wo = -normalize(p.d);
+  V3 wi, f;
+  float pdf = 0.0f;
+  if (!mat_sample(S, m, rec, wo, wi, pdf, f, g)) return false;
+  Path c;
+  c.o = rec.p, c.d = wi, c.depth = p.depth + 1;
+  if (m.kind != RTX_MAT_LAMBERTIAN) {  // IsSpecular
+    c.thr = p.thr * f;
+  } else {
+    if (pdf < 1e-6f) return false;
+    float ct = fmaxf(0.0f, (float)dot(wi, rec.normal));
+    c.thr = ((double)ct * (p.thr * f)) / (double)pdf;
+  }
+  if (c.depth > 5) {  // Russian roulette (wavefront.cc:189-205)
+    double q = fmax(fmax(c.thr.x, c.thr.y), c.thr.z);
+    q = q < 0.1 ? 0.1 : (q > 0.95 ? 0.95 : q);
+    if (g.next() > q) return false;
+    c.thr = c.thr / q;
+  }
+  c.draw = g.draw;
+  p = c;
+  return true;
+}
+
+}  // namespace rtxd

@@ -1,0 +1,423 @@
+// rtx_kernels.h — HIP kernels of the hot path (included once, by rtx_capi.hip).
+//
+//   k_intersect        RayIntegrator::IntersectBatch seam (one ray per lane)
+//   k_wf_generate      WavefrontRenderer primary generation (wavefront.cc:62-79)
+//   k_wf_extend        closest hit for every queued path (traversal only: low VGPR count,
+//                      high occupancy for the latency-bound BVH walk)
+//   k_wf_shade         shading + Russian roulette + ballot-compacted child queue
+//   k_persistent       persistent lanes with per-wave refill (same results as the wavefront)
+//   k_accumulate       RecordSample/IsConverged in sample order (pixel_state.h:22-72)
+//   k_resolve          sum/(float)samples (wavefront.cc:229-235) or pixel/N (mega_kernel)
+//
+// Sample bookkeeping: a render is processed in groups of K samples per pixel.  Every path
+// (pixel p, sample s0+k) owns slot p*K+k of Lbuf and writes its radiance exactly once, so
+// k_accumulate can replay RecordSample in sample order: the result equals the reference's
+// pass-by-pass order regardless of how lanes, queues or XCDs interleave the work.
+#pragma once
+
+#include "rtx_device.h"
+
+namespace rtxd {
+
+constexpr int kBlock = 256;
+
+#ifndef RTX_TRACE_WAVES
+#define RTX_TRACE_WAVES 2  // min waves per SIMD requested for the trace kernels
+#endif
+
+// Pixel subset of the image handled by one call (rectangle or interleaved row stripes).
+struct PixelMap {
+  int32_t W, H;
+  int32_t stripes;  // 0: rectangle, 1: stripes
+  int32_t x0, y0, w, h;
+  int32_t srows, sidx, scount;
+  __device__ __forceinline__ void xy(int64_t local, int& x, int& y) const {
+    if (!stripes) {
+      x = x0 + (int)(local % w);
+      y = y0 + (int)(local / w);
+    } else {
+      int r = (int)(local / W);
+      x = (int)(local % W);
+      int blk = r / srows;
+      y = (blk * scount + sidx) * srows + r % srows;
+    }
+  }
+};
+
+struct PathQueue {  // SoA, one entry per in-flight path
+  double *ox, *oy, *oz, *dx, *dy, *dz, *tx, *ty, *tz;
+  uint32_t* slot;
+  uint32_t* meta;  // depth << 24 | draw
+  int32_t* hit;    // closest primitive (leaf order) or -1, written by k_wf_extend
+};
+
+struct RenderArgs {
+  DScene S;
+  rtx_camera cam;
+  PixelMap map;
+  uint64_t seed;
+  int64_t npix;         // pixels in the subset
+  int32_t K;            // samples in this group
+  int32_t s0;           // first sample index of the group
+  int32_t max_depth;
+  int32_t scatter_api;  // megakernel (Scatter/GetPixel) semantics
+  const uint8_t* conv;  // per-pixel converged flag (adaptive), may be null
+  double* L;            // Lbuf: 3 doubles per slot
+  unsigned long long* counters;  // [0] segments [1] primaries [2] node visits [3] prim tests
+};
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+// Wave-level compaction: this lane's destination among the lanes with `want` set; one
+// atomicAdd per wave (ballot + popcount of the lower lanes).
+__device__ __forceinline__ int64_t wave_compact(bool want, unsigned int* counter) {
+  const unsigned long long mask = __ballot(want);
+  if (mask == 0) return -1;
+  const int leader = __ffsll((long long)mask) - 1;
+  const int total = __popcll(mask);
+  unsigned int base = 0;
+  if ((int)lane_id() == leader) base = atomicAdd(counter, (unsigned int)total);
+  base = __shfl(base, leader);
+  const int rank = __popcll(mask & ((1ull << lane_id()) - 1ull));
+  return want ? (int64_t)base + rank : -1;
+}
+
+template <int STACK, bool FAST, bool COUNT>
+__device__ __forceinline__ int64_t trace(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
+                                         Counters& c) {
+  if (FAST) return trace_fast<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c);
+  return trace_parity<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c);
+}
+
+__device__ __forceinline__ void flush_counters(const RenderArgs& A, const Counters& c, uint32_t segs,
+                                               uint32_t prims, bool count) {
+  if (count) {
+    atomicAdd(&A.counters[2], (unsigned long long)c.nodes);
+    atomicAdd(&A.counters[3], (unsigned long long)c.prims);
+  }
+  if (segs) atomicAdd(&A.counters[0], (unsigned long long)segs);
+  if (prims) atomicAdd(&A.counters[1], (unsigned long long)prims);
+}
+
+// ---------------------------------------------------------------------------------------
+// IntersectBatch
+// ---------------------------------------------------------------------------------------
+template <int STACK, bool FAST>
+__global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_intersect(DScene S, const rtx_ray* __restrict__ rays,
+                                                                       int64_t n, rtx_hit* __restrict__ hits,
+                                                                       double tmin, double tmax) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* stk = lds + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const rtx_ray r = rays[i];
+  V3 o{r.origin[0], r.origin[1], r.origin[2]}, d{r.direction[0], r.direction[1], r.direction[2]};
+  Counters c{0, 0};
+  const int64_t best = trace<STACK, FAST, false>(S, o, d, tmin, tmax, stk, c);
+  rtx_hit out;
+  out.pad_ = 0;
+  if (best >= 0) {
+    Hit h;
+    finish_hit(S, best, o, d, tmin, h);
+    out.hit = 1;
+    out.front_face = h.front_face, out.material = h.mat, out.t = h.t;
+    out.p[0] = h.p.x, out.p[1] = h.p.y, out.p[2] = h.p.z;
+    out.normal[0] = h.normal.x, out.normal[1] = h.normal.y, out.normal[2] = h.normal.z;
+    out.u = h.u, out.v = h.v;
+  } else {
+    out.hit = 0, out.front_face = 0, out.material = -1, out.t = 0;
+    out.p[0] = out.p[1] = out.p[2] = 0;
+    out.normal[0] = out.normal[1] = out.normal[2] = 0;
+    out.u = out.v = 0;
+  }
+  hits[i] = out;
+}
+
+// ---------------------------------------------------------------------------------------
+// Wavefront: primary generation for every slot of active pixels
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_wf_generate(RenderArgs A, PathQueue q, unsigned int* count) {
+  const int64_t nslots = A.npix * A.K;
+  uint32_t made = 0;
+  for (int64_t base = (int64_t)blockIdx.x * kBlock; base < nslots; base += (int64_t)gridDim.x * kBlock) {
+    const int64_t slot = base + threadIdx.x;
+    bool live = slot < nslots;
+    int64_t p = live ? slot / A.K : 0;
+    if (live && A.conv && A.conv[p]) live = false;
+    Path P;
+    if (live) {
+      const int k = (int)(slot - p * A.K);
+      int x, y;
+      A.map.xy(p, x, y);
+      Rng g = make_rng(A.seed, (uint32_t)(y * A.map.W + x), (uint32_t)(A.s0 + k), 0u);
+      get_ray(A.cam, x, y, g, P.o, P.d);
+      P.draw = g.draw;
+      made++;
+    }
+    const int64_t dst = wave_compact(live, count);
+    if (live) {
+      q.ox[dst] = P.o.x, q.oy[dst] = P.o.y, q.oz[dst] = P.o.z;
+      q.dx[dst] = P.d.x, q.dy[dst] = P.d.y, q.dz[dst] = P.d.z;
+      q.tx[dst] = 1.0, q.ty[dst] = 1.0, q.tz[dst] = 1.0;
+      q.slot[dst] = (uint32_t)slot;
+      q.meta[dst] = P.draw;  // depth 0
+    }
+  }
+  flush_counters(A, Counters{0, 0}, 0, made, false);
+}
+
+// Closest hit for every queued path (one ray per lane, grid-stride).
+template <int STACK, bool FAST, bool COUNT>
+__global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_wf_extend(RenderArgs A, PathQueue q,
+                                                                       const unsigned int* count) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* stk = lds + threadIdx.x;
+  const int64_t n = *count;
+  Counters c{0, 0};
+  uint32_t segs = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
+    const V3 o = v3(q.ox[i], q.oy[i], q.oz[i]);
+    const V3 d = v3(q.dx[i], q.dy[i], q.dz[i]);
+    q.hit[i] = (int32_t)trace<STACK, FAST, COUNT>(A.S, o, d, (double)0.001f, kInf, stk, c);
+    segs++;
+  }
+  flush_counters(A, c, segs, 0, COUNT);
+}
+
+// Shading for every queued path + compacted child queue (wavefront.cc:109-217).
+__global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in, const unsigned int* in_count,
+                                                     PathQueue out, unsigned int* out_count) {
+  const int64_t n = *in_count;
+  for (int64_t base = (int64_t)blockIdx.x * kBlock; base < n; base += (int64_t)gridDim.x * kBlock) {
+    const int64_t i = base + threadIdx.x;
+    bool cont = false;
+    Path P;
+    uint32_t slot = 0;
+    if (i < n) {
+      P.o = v3(in.ox[i], in.oy[i], in.oz[i]);
+      P.d = v3(in.dx[i], in.dy[i], in.dz[i]);
+      P.thr = v3(in.tx[i], in.ty[i], in.tz[i]);
+      slot = in.slot[i];
+      const uint32_t meta = in.meta[i];
+      P.depth = (int32_t)(meta >> 24);
+      P.draw = meta & 0xFFFFFFu;
+      const int64_t p = slot / A.K;
+      const int k = (int)(slot - p * A.K);
+      int x, y;
+      A.map.xy(p, x, y);
+      const int32_t best = in.hit[i];
+      Hit h;
+      if (best >= 0) finish_hit<false>(A.S, best, P.o, P.d, (double)0.001f, h);
+      Rng g = make_rng(A.seed, (uint32_t)(y * A.map.W + x), (uint32_t)(A.s0 + k), P.draw);
+      V3 L;
+      cont = shade(A.S, A.max_depth, P, h, best >= 0, g, L);
+      if (!cont) {
+        double* Lp = A.L + 3 * (int64_t)slot;
+        Lp[0] = L.x, Lp[1] = L.y, Lp[2] = L.z;
+      }
+    }
+    const int64_t dst = wave_compact(cont, out_count);
+    if (cont) {
+      out.ox[dst] = P.o.x, out.oy[dst] = P.o.y, out.oz[dst] = P.o.z;
+      out.dx[dst] = P.d.x, out.dy[dst] = P.d.y, out.dz[dst] = P.d.z;
+      out.tx[dst] = P.thr.x, out.ty[dst] = P.thr.y, out.tz[dst] = P.thr.z;
+      out.slot[dst] = slot;
+      out.meta[dst] = ((uint32_t)P.depth << 24) | (P.draw & 0xFFFFFFu);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Persistent lanes: each lane owns one path at a time and refills from a global slot
+// counter in wave-sized chunks (one atomic per kChunk slots), so lanes whose path ended
+// (miss, emitter, absorption, Russian roulette) are immediately given a new primary —
+// the per-wave __ballot of idle lanes is the active-ray compaction.
+// ---------------------------------------------------------------------------------------
+constexpr int kChunk = 256;
+
+template <int STACK, bool FAST, bool COUNT, bool SCATTER>
+__global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderArgs A, unsigned long long* next_slot) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* stk = lds + threadIdx.x;
+  const uint64_t nslots = (uint64_t)A.npix * (uint64_t)A.K;
+  // GetPixel uses Interval(0.001, inf) (camera.h:158); IntersectBatch uses 0.001f (cpu_ray_integrator.h:21)
+  const double tmin = SCATTER ? 0.001 : (double)0.001f;
+  Counters c{0, 0};
+  uint32_t segs = 0, prims = 0;
+  uint64_t chunk_base = 0, chunk_left = 0;  // wave-uniform
+  bool exhausted = false;                   // wave-uniform
+  bool has = false;
+  Path P;
+  P.depth = 0, P.draw = 0;
+  uint64_t slot = 0;
+  int x = 0, y = 0, k = 0;
+  const unsigned long long lt = (1ull << lane_id()) - 1ull;
+  while (true) {
+    // ---- refill: ballot of idle lanes, leftover of the current chunk first ----
+    const unsigned long long idle = __ballot(!has);
+    bool fresh = false;
+    if (idle != 0 && !exhausted) {
+      const uint64_t nidle = (uint64_t)__popcll(idle);
+      const uint64_t rank = (uint64_t)__popcll(idle & lt);
+      if (chunk_left >= nidle) {
+        if (!has) slot = chunk_base + rank, fresh = true;
+        chunk_base += nidle, chunk_left -= nidle;
+      } else {
+        unsigned long long nb = 0;
+        if (lane_id() == 0) nb = atomicAdd(next_slot, (unsigned long long)kChunk);
+        nb = __shfl(nb, 0);
+        if (!has) {
+          if (rank < chunk_left) slot = chunk_base + rank, fresh = true;
+          else if (nb < nslots) slot = nb + (rank - chunk_left), fresh = true;
+        }
+        if (nb < nslots) {
+          const uint64_t used = nidle - chunk_left;
+          chunk_base = nb + used, chunk_left = kChunk - used;
+        } else {
+          chunk_left = 0, exhausted = true;
+        }
+      }
+    }
+    // ---- start the primary path of a freshly assigned slot ----
+    if (fresh && slot < nslots) {
+      const int64_t p = (int64_t)(slot / (uint64_t)A.K);
+      if (!(A.conv && A.conv[p])) {
+        k = (int)(slot - (uint64_t)p * A.K);
+        A.map.xy(p, x, y);
+        Rng g = make_rng(A.seed, (uint32_t)(y * A.map.W + x), (uint32_t)(A.s0 + k), 0u);
+        get_ray(A.cam, x, y, g, P.o, P.d);
+        P.draw = g.draw;
+        P.thr = v3(1.0, 1.0, 1.0);
+        P.depth = SCATTER ? A.max_depth : 0;
+        has = true;
+        prims++;
+      }
+    }
+    if (!__any(has)) {
+      if (exhausted) break;
+      continue;
+    }
+    if (!has) continue;
+    // ---- one segment: closest hit + shading ----
+    V3 L;
+    bool cont;
+    if (SCATTER && P.depth <= 0) {  // GetPixel: depth exhausted -> black (camera.h:149-151)
+      L = v3(0, 0, 0);
+      cont = false;
+    } else {
+      const int64_t best = trace<STACK, FAST, COUNT>(A.S, P.o, P.d, tmin, kInf, stk, c);
+      segs++;
+      Rng g = make_rng(A.seed, (uint32_t)(y * A.map.W + x), (uint32_t)(A.s0 + k), P.draw);
+      Hit h;
+      if (best >= 0) finish_hit<false>(A.S, best, P.o, P.d, tmin, h);
+      if (SCATTER) {
+        // GetPixel(r, depth) iteratively (camera.h:148-174); P.thr holds the product of the
+        // attenuations, P.depth the remaining depth.  Emitters never scatter, so the
+        // recursion's emitted terms reduce to the terminal one.
+        if (best < 0) {
+          L = P.thr * sky(P.d);
+          cont = false;
+        } else {
+          const rtx_material m = A.S.mats[h.mat];
+          V3 att, sd;
+          if (mat_scatter(A.S, m, P.d, h, att, sd, g)) {
+            P.thr = P.thr * att;
+            P.o = h.p, P.d = sd;
+            P.depth--;
+            P.draw = g.draw;
+            cont = true;
+          } else {
+            L = P.thr * mat_emitted(A.S, m, h);
+            cont = false;
+          }
+        }
+      } else {
+        cont = shade(A.S, A.max_depth, P, h, best >= 0, g, L);
+      }
+    }
+    if (!cont) {
+      double* Lp = A.L + 3 * (int64_t)slot;
+      Lp[0] = L.x, Lp[1] = L.y, Lp[2] = L.z;
+      has = false;
+    }
+  }
+  flush_counters(A, c, segs, prims, COUNT);
+}
+
+// ---------------------------------------------------------------------------------------
+// RecordSample in sample order (pixel_state.h:22-39) + IsConverged (pixel_state.h:54-72)
+// ---------------------------------------------------------------------------------------
+struct PixelSoA {
+  double *sum, *mean, *m2;  // 3 x npix each (channel-major)
+  int32_t* samples;
+  uint8_t* conv;
+};
+
+__global__ __launch_bounds__(kBlock) void k_accumulate(PixelSoA px, const double* __restrict__ L, int64_t npix,
+                                                       int K, int adaptive, int min_spp, double rel) {
+  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (p >= npix) return;
+  if (px.conv[p]) return;
+  double sum[3], mean[3], m2[3];
+  for (int c = 0; c < 3; c++) sum[c] = px.sum[c * npix + p], mean[c] = px.mean[c * npix + p], m2[c] = px.m2[c * npix + p];
+  int n = px.samples[p];
+  bool conv = false;
+  const int need = adaptive ? min_spp : 0x7FFFFFFF;
+  for (int k = 0; k < K && !conv; k++) {
+    const double* x = L + 3 * (p * K + k);
+    n++;
+    for (int c = 0; c < 3; c++) {
+      double mu = mean[c];
+      double delta = x[c] - mu;
+      mu += delta / n;
+      double delta2 = x[c] - mu;
+      mean[c] = mu;
+      m2[c] += delta2 * delta;
+    }
+    for (int c = 0; c < 3; c++) sum[c] += x[c];
+    if (n >= need) {
+      bool ok = true;
+      for (int c = 0; c < 3 && ok; c++) {
+        double var = n > 1 ? m2[c] / (n - 1) : 0.0;
+        double mu = fmax(fabs(mean[c]), 1e-3);
+        double err = sqrt(var) / sqrt((double)n);
+        if (err / mu > rel) ok = false;
+      }
+      conv = ok;
+    }
+  }
+  for (int c = 0; c < 3; c++) px.sum[c * npix + p] = sum[c], px.mean[c * npix + p] = mean[c], px.m2[c * npix + p] = m2[c];
+  px.samples[p] = n;
+  px.conv[p] = conv;
+}
+
+// Fixed-spp megakernel accumulation: DefaultSampler sums GetPixel results in sample order.
+__global__ __launch_bounds__(kBlock) void k_accumulate_sum(PixelSoA px, const double* __restrict__ L, int64_t npix,
+                                                           int K) {
+  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (p >= npix) return;
+  double sum[3];
+  for (int c = 0; c < 3; c++) sum[c] = px.sum[c * npix + p];
+  for (int k = 0; k < K; k++) {
+    const double* x = L + 3 * (p * K + k);
+    for (int c = 0; c < 3; c++) sum[c] += x[c];
+  }
+  for (int c = 0; c < 3; c++) px.sum[c * npix + p] = sum[c];
+  px.samples[p] += K;
+}
+
+// wavefront.cc:229-235: sum / (float)samples  (Vec3 operator/ is (1/t)*v); megakernel
+// (mega_kernel.h + sampler.h:32): pixel /= num_samples.
+__global__ __launch_bounds__(kBlock) void k_resolve(PixelSoA px, int64_t npix, int megakernel, int spp,
+                                                    double* __restrict__ rgb, int32_t* __restrict__ spp_out) {
+  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (p >= npix) return;
+  const int n = px.samples[p];
+  double s = 0.0;
+  if (megakernel) s = 1.0 / (double)spp;
+  else if (n > 0) s = 1.0 / (double)(float)n;
+  for (int c = 0; c < 3; c++) rgb[3 * p + c] = (megakernel || n > 0) ? s * px.sum[c * npix + p] : 0.0;
+  if (spp_out) spp_out[p] = megakernel ? spp : n;
+}
+
+}  // namespace rtxd

@@ -1,0 +1,117 @@
+// renderer.cc — GpuRayIntegrator, WavefrontRenderer and MegaKernel over the C ABI.
+#include <stdexcept>
+
+#include "rt/material.h"
+#include "rt/renderer.h"
+
+namespace rt::integrator {
+
+namespace {
+void check(int rc, const char* what) {
+  if (rc != RTX_OK) throw std::runtime_error(std::string(what) + ": " + rtx_last_error());
+}
+}  // namespace
+
+GpuRayIntegrator::GpuRayIntegrator(const scene::Scene* world, int device, int precision)
+    : world_(world), device_(device), precision_(precision) {
+  if (!world_) throw std::invalid_argument("GpuRayIntegrator: world is null");
+  flat_ = scene::Flatten(*world_);
+  const rtx_scene_desc d = flat_.desc();
+  check(rtx_scene_create(device_, &d, &dev_), "rtx_scene_create");
+}
+
+GpuRayIntegrator::~GpuRayIntegrator() { rtx_scene_destroy(dev_); }
+
+// cpu_ray_integrator.h:18-46 contract on the GPU: [0.001f, +inf), hit flag per record,
+// HitRecord::mat re-attached from the material id.
+void GpuRayIntegrator::IntersectBatch(const std::vector<core::Ray>& rays, std::vector<geom::HitRecord>& hits) const {
+  hits.resize(rays.size());
+  if (rays.empty()) return;
+  std::vector<rtx_ray> r(rays.size());
+  for (size_t i = 0; i < rays.size(); i++)
+    for (int k = 0; k < 3; k++) r[i].origin[k] = rays[i].origin()[k], r[i].direction[k] = rays[i].direction()[k];
+  std::vector<rtx_hit> h(rays.size());
+  check(rtx_intersect(dev_, r.data(), r.size(), h.data(), RTX_SEAM_TMIN, core::kInfinity, precision_),
+        "rtx_intersect");
+  for (size_t i = 0; i < rays.size(); i++) {
+    geom::HitRecord& o = hits[i];
+    o.hit = h[i].hit != 0;
+    if (!o.hit) {
+      o.mat.reset();
+      continue;
+    }
+    o.t = h[i].t;
+    o.p = core::Point3(h[i].p[0], h[i].p[1], h[i].p[2]);
+    o.normal = core::Vec3(h[i].normal[0], h[i].normal[1], h[i].normal[2]);
+    o.front_face = h[i].front_face != 0;
+    o.u = h[i].u, o.v = h[i].v;
+    o.mat = flat_.material_ptrs.at(h[i].material);
+  }
+}
+
+}  // namespace rt::integrator
+
+namespace rt::renderer {
+
+rtx_render_params DefaultParams(int spp, int max_depth) {
+  rtx_render_params p{};
+  p.spp = spp;
+  p.max_depth = max_depth;
+  p.adaptive = 1;
+  p.min_spp = 16;                        // wavefront.cc:43
+  p.rel_threshold = (double)0.05f;       // wavefront.cc:42 (const float)
+  p.seed = 1234;
+  p.mode = RTX_MODE_WAVEFRONT;
+  p.precision = RTX_PREC_PARITY;
+  return p;
+}
+
+WavefrontRenderer::WavefrontRenderer(const scene::Scene& w, const scene::Camera& c, integrator::RayIntegrator& i,
+                                     int max_depth, int max_samples, int /*batch_size*/)
+    : world(w), cam(c), integrator(i), params_(DefaultParams(max_samples, max_depth)) {}
+
+void WavefrontRenderer::Render() { Render(std::cout); }
+
+void WavefrontRenderer::Render(std::ostream& out) {
+  auto* gpu = dynamic_cast<integrator::GpuRayIntegrator*>(&integrator);
+  if (!gpu)
+    throw std::invalid_argument(
+        "WavefrontRenderer (MI355X): the integrator must be a GpuRayIntegrator; shading runs on the device");
+  const rtx_camera& dc = cam.device();
+  if (dc.image_width <= 0) throw std::invalid_argument("WavefrontRenderer: camera not initialised");
+  rtx_render_params p = params_;
+  p.x0 = p.y0 = p.w = p.h = 0;
+  p.stripe_rows = 0;
+  const int64_t n = (int64_t)dc.image_width * dc.image_height;
+  rgb_.assign(3 * n, 0.0);
+  spp_.assign(n, 0);
+  if (rtx_render(gpu->device_scene(), &dc, &p, rgb_.data(), spp_.data(), &stats_) != RTX_OK)
+    throw std::runtime_error(std::string("rtx_render: ") + rtx_last_error());
+  // wavefront.cc:238-241
+  out << "P3\n" << dc.image_width << ' ' << dc.image_height << "\n255\n";
+  for (int64_t k = 0; k < n; k++) core::write_color(out, core::Color(rgb_[3 * k], rgb_[3 * k + 1], rgb_[3 * k + 2]));
+}
+
+MegaKernel::MegaKernel(scene::Scene& scene, scene::Camera& camera, integrator::Sampler& sampler, int device)
+    : sampler_(sampler), world_(scene), cam_(camera), device_(device) {}
+
+void MegaKernel::Render() { Render(std::cout); }
+
+void MegaKernel::Render(std::ostream& out) {
+  cam_.Initialize();  // mega_kernel.h:16
+  integrator::GpuRayIntegrator gpu(&world_, device_);
+  const rtx_camera& dc = cam_.device();
+  rtx_render_params p = DefaultParams(sampler_.num_samples(), cam_.max_depth_);
+  p.adaptive = 0;
+  p.mode = RTX_MODE_MEGAKERNEL;
+  p.seed = seed_;
+  const int64_t n = (int64_t)dc.image_width * dc.image_height;
+  rgb_.assign(3 * n, 0.0);
+  rtx_stats st{};
+  if (rtx_render(gpu.device_scene(), &dc, &p, rgb_.data(), nullptr, &st) != RTX_OK)
+    throw std::runtime_error(std::string("rtx_render: ") + rtx_last_error());
+  out << "P3\n" << dc.image_width << ' ' << dc.image_height << "\n255\n";
+  for (int64_t k = 0; k < n; k++) core::write_color(out, core::Color(rgb_[3 * k], rgb_[3 * k + 1], rgb_[3 * k + 2]));
+}
+
+}  // namespace rt::renderer

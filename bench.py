@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""bench.py — Mrays/s of the MI355X path-tracing hot path (BASELINE.json metric).
+
+A "step" is one complete frame of the workload (every sample of every pixel of this rank's
+shard) rendered through the C ABI (rtx_render_device into device-resident buffers, scene
+already in HBM).  Default workload = BASELINE configs[1]: C2 final_scene, 1200x675,
+100 spp, depth 50, fixed spp (adaptive sampling off).
+
+N GPUs (one process per GPU, launched by torch.distributed.run): the image's rows are
+split into interleaved 8-row stripes (stripe k -> rank k mod N) and the sample
+count is N x spp, so every rank traces the same amount of work as the 1-GPU run ("weak"
+scaling); no collective touches the data path (RCCL only carries the timing barrier and
+the max-over-ranks reduction).
+
+Prints ONE JSON line (rank 0).  `roofline` uses the dominant kernel's average launch time
+(HIP events on the library's stream, over the timed region) and the algorithmic bytes per
+launch from a separate counting pass (DESIGN.md "Roofline accounting").  `cpu_baseline`
+times the CPU oracle (oracle/librtx_oracle.so, the restatement pinned to the reference) on
+a bounded crop of the same workload on this host's cores, and `rms_vs_cpu` compares the
+GPU and CPU pixels of that crop at the same seed.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "3360-ray-tracer_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+WORKLOADS = {  # name -> (scene recipe, camera preset, width, spp, depth)
+    "c2_final": ("final", "c2_final", 1200, 100, 50),
+    "c3_bunny": ("bunny", "c3_bunny", 1000, 200, 20),
+    "c1_three": ("three", "c1_three", 400, 4, 4),
+    "c4_bunny4k": ("bunny", "c4_bunny4k", 3840, 1024, 50),
+    "c5_mixed": ("mixed", "c5_mixed", 3840, 2048, 50),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+STRIPE_ROWS = 8
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workload", default="c2_final", choices=sorted(WORKLOADS))
+    ap.add_argument("--spp", type=int, default=0, help="override samples per pixel (per GPU)")
+    ap.add_argument("--mode", default="persistent", choices=["wavefront", "persistent"])
+    ap.add_argument("--precision", default="fast", choices=["parity", "fast"])
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    import rtx
+
+    scene_name, preset, width, spp, depth = WORKLOADS[args.workload]
+    spp = args.spp or spp
+    total_spp = spp * world  # weak scaling: N x samples over 1/N of the pixels
+    host = rtx.HostScene.recipe(scene_name, 1234)
+    dev = rtx.DeviceScene(host, device=local if world > 1 else 0)
+    cam = rtx.camera(rtx.camera_config(preset, width=width))
+    p = rtx.RenderParams()
+    p.spp, p.max_depth, p.adaptive, p.seed = total_spp, depth, 0, args.seed
+    p.mode, p.precision = rtx.MODES[args.mode], rtx.PRECISIONS[args.precision]
+    if world > 1:
+        p.stripe_rows, p.stripe_index, p.stripe_count = STRIPE_ROWS, rank, world
+    npix = rtx.lib().rtx_render_pixel_count(cam, p)
+
+    import torch
+
+    dev_id = local if world > 1 else 0
+    d_rgb = torch.empty((npix, 3), dtype=torch.float64, device=f"cuda:{dev_id}")
+    d_spp = torch.empty((npix,), dtype=torch.int32, device=f"cuda:{dev_id}")
+
+    def step():
+        return dev.render_device(cam, p, d_rgb.data_ptr(), d_spp.data_ptr())
+
+    for _ in range(args.warmup):
+        step()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    t0 = time.perf_counter()
+    stats = [step() for _ in range(args.steps)]
+    barrier()
+    elapsed = time.perf_counter() - t0
+    rays = sum(s["rays_total"] for s in stats)
+    hot_ms = sum(s["hot_kernel_ms"] for s in stats)
+    hot_launches = sum(s["hot_launches"] for s in stats)
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev_id}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor([rays], dtype=torch.float64, device=f"cuda:{dev_id}")
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        rays_all = float(r.item())
+    else:
+        rays_all = float(rays)
+
+    # counting pass (diagnostic kernel build) for algorithmic bytes per segment
+    p.flags = 1
+    cst = step()
+    p.flags = 0
+    segs = max(1, cst["rays_total"])
+    nodes_per_seg = cst["node_visits"] / segs
+    prims_per_seg = cst["prim_tests"] / segs
+    node_bytes = 64  # fast: FNode (2 f32 child boxes); parity: rtx_bvh_node (f64 box) — both 64 B
+    prim_bytes = 80  # rtx_prim (f64 geometry + kind/material)
+    state_bytes = 48 if args.mode == "persistent" else 48 + 88 + 88  # material 48 (+ SoA path state in/out)
+    bytes_per_seg = node_bytes * nodes_per_seg + prim_bytes * prims_per_seg + state_bytes
+    segs_per_launch = rays / max(1, hot_launches)
+    avg_launch_s = hot_ms / 1e3 / max(1, hot_launches)
+    achieved_gbs = bytes_per_seg * segs_per_launch / avg_launch_s / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", f"traffic_{args.workload}_{args.mode}_{args.precision}.json")
+    if os.path.exists(tf):
+        traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
+
+    out = None
+    if rank == 0:
+        out = {
+            "metric": "Mrays/s (primary+secondary) at fixed spp; RMS pixel error vs CPU ref",
+            "value": rays_all / elapsed / 1e6,
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": f"{args.workload}: {scene_name} scene {width}x{cam.image_height}, "
+                                   f"{spp} spp/GPU-share, depth {depth}, fixed spp",
+                       "scene_prims": int(host.desc().n_prims), "bvh_nodes": int(host.desc().n_nodes),
+                       "mode": args.mode, "precision": args.precision, "spp_total": total_spp,
+                       "pixels_per_rank": int(npix), "stripe_rows": STRIPE_ROWS if world > 1 else None,
+                       "parallelism": f"tile-split x{world} (interleaved row stripes, no collectives)"},
+            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_persistent" if args.mode == "persistent" else "k_wf_bounce",
+                         "avg_launch_ms": avg_launch_s * 1e3, "segments_per_launch": segs_per_launch,
+                         "bytes_per_segment": bytes_per_seg, "nodes_per_segment": nodes_per_seg,
+                         "prims_per_segment": prims_per_seg},
+            "rays_per_step": rays_all / args.steps,
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"], out["rms_vs_cpu"] = cpu_baseline(rtx, dev, host, cam, preset, spp, depth, args)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(rtx, dev, host, cam, preset, spp, depth, args):
+    """Time the CPU oracle on a centred crop of the same workload; compare its pixels."""
+    import tempfile
+
+    import oracle_ctypes as orc
+
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    W, H = cam.image_width, cam.image_height
+    cw, ch = max(1, W // 8), max(1, H // 8)
+    tile = (W // 2 - cw // 2, H // 2 - ch // 2, cw, ch)
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "scene.rtxs")
+        host.write(path)
+        s = orc.Scene(path)
+        cfg = orc.camera_preset(preset)
+        t0 = time.perf_counter()
+        ref, _, st = s.render(cfg, W, spp, depth, args.seed, adaptive=0, rng="philox", mode="per_pixel", tile=tile,
+                              threads=threads)
+        dt = time.perf_counter() - t0
+    gpu, _, _ = dev.render(cam, spp, depth, seed=args.seed, adaptive=False, tile=tile, mode="wavefront",
+                           precision="parity")
+    rms = float(np.sqrt(np.mean((gpu - ref.reshape(-1, 3)) ** 2)))
+    base = {"value": st["rays"] / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"centre crop {cw}x{ch} of the same frame, {spp} spp, depth {depth}, "
+                      f"{st['rays']} segments in {dt:.1f}s (oracle/rtx_oracle.cc, OpenMP, philox)"}
+    return base, rms
+
+
+if __name__ == "__main__":
+    main()
