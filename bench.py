@@ -59,12 +59,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # torch (plumbing: device buffers, barrier, max-over-ranks) must initialise its HIP
+    # runtime before librtx.so is loaded into the process
+    import torch
+
     dist = None
+    torch.cuda.init()
+    torch.cuda.set_device(local if world > 1 else 0)
     if world > 1:
-        import torch
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
         dist.init_process_group("nccl")
 
     import rtx
@@ -81,8 +85,6 @@ def main():
     if world > 1:
         p.stripe_rows, p.stripe_index, p.stripe_count = STRIPE_ROWS, rank, world
     npix = rtx.lib().rtx_render_pixel_count(cam, p)
-
-    import torch
 
     dev_id = local if world > 1 else 0
     d_rgb = torch.empty((npix, 3), dtype=torch.float64, device=f"cuda:{dev_id}")
@@ -182,13 +184,21 @@ def cpu_baseline(rtx, dev, host, cam, preset, spp, depth, args):
 
     threads = args.cpu_threads or min(16, os.cpu_count() or 1)
     W, H = cam.image_width, cam.image_height
-    cw, ch = max(1, W // 8), max(1, H // 8)
-    tile = (W // 2 - cw // 2, H // 2 - ch // 2, cw, ch)
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "scene.rtxs")
         host.write(path)
         s = orc.Scene(path)
         cfg = orc.camera_preset(preset)
+        # probe on a small centre crop, then size the timed sample to ~10 s of CPU work
+        # (capped at the whole frame): full-width bands of rows around the image centre
+        probe = (0, H // 2 - 2, W, 4)
+        t0 = time.perf_counter()
+        s.render(cfg, W, spp, depth, args.seed, adaptive=0, rng="philox", mode="per_pixel", tile=probe,
+                 threads=threads)
+        per_row = (time.perf_counter() - t0) / 4
+        ch = int(max(4, min(H, 10.0 / max(per_row, 1e-6))))
+        cw = W
+        tile = (0, max(0, H // 2 - ch // 2), cw, ch)
         t0 = time.perf_counter()
         ref, _, st = s.render(cfg, W, spp, depth, args.seed, adaptive=0, rng="philox", mode="per_pixel", tile=tile,
                               threads=threads)
@@ -197,7 +207,7 @@ def cpu_baseline(rtx, dev, host, cam, preset, spp, depth, args):
                            precision="parity")
     rms = float(np.sqrt(np.mean((gpu - ref.reshape(-1, 3)) ** 2)))
     base = {"value": st["rays"] / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"centre crop {cw}x{ch} of the same frame, {spp} spp, depth {depth}, "
+            "sample": f"centre band {cw}x{ch} of the same {W}x{H} frame, {spp} spp, depth {depth}, "
                       f"{st['rays']} segments in {dt:.1f}s (oracle/rtx_oracle.cc, OpenMP, philox)"}
     return base, rms
 

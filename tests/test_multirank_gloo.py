@@ -1,0 +1,78 @@
+"""N>1 path on CPU: world_size-2 `gloo` ranks, each rendering its interleaved row stripes
+(the bench's partition) with the CPU oracle; the gathered image must equal the
+single-process render bit for bit (the RNG is keyed by the global pixel), and the
+max-over-ranks timing reduction must pick the slowest rank."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+from conftest import ROOT, scene_path  # noqa: E402
+
+STRIPE_ROWS = 8
+W, SPP, DEPTH, SEED = 40, 3, 50, 2024
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def stripe_rows(h, rows, idx, count):
+    return [y for y in range(h) if (y // rows) % count == idx]
+
+
+def worker(rank, world, port, out_dir):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ctypes as orc
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = orc.camera_preset("c2_final")
+    s = orc.Scene(scene_path("final"))
+    H = orc.make_camera(cfg, W).height
+    rows = stripe_rows(H, STRIPE_ROWS, rank, world)
+    mine = np.zeros((H, W, 3))
+    for y in rows:  # contiguous rows of a stripe rendered as 1-row tiles
+        fb, _, _ = s.render(cfg, W, SPP, DEPTH, SEED, adaptive=0, rng="philox", mode="per_pixel", tile=(0, y, W, 1))
+        mine[y] = fb[0]
+    t = torch.from_numpy(mine)
+    gathered = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(gathered, t)
+    elapsed = torch.tensor([float(rank + 1)], dtype=torch.float64)  # rank r "took" r+1 s
+    dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        img = sum(g.numpy() for g in gathered)
+        np.save(os.path.join(out_dir, "img.npy"), img)
+        np.save(os.path.join(out_dir, "tmax.npy"), elapsed.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_stripes_match_single_process(tmp_path, orc):
+    world = 2
+    mp.spawn(worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    img = np.load(tmp_path / "img.npy")
+    cfg = orc.camera_preset("c2_final")
+    full, _, _ = orc.Scene(scene_path("final")).render(cfg, W, SPP, DEPTH, SEED, adaptive=0, rng="philox",
+                                                       mode="per_pixel", threads=2)
+    assert np.array_equal(img, full)
+    assert np.load(tmp_path / "tmax.npy")[0] == 2.0
+
+
+def test_stripes_cover_every_row_once():
+    for h in (1, 7, 36, 675, 2160):
+        for n in (1, 2, 3, 4, 8):
+            rows = sorted(sum((stripe_rows(h, STRIPE_ROWS, k, n) for k in range(n)), []))
+            assert rows == list(range(h))
+            sizes = [len(stripe_rows(h, STRIPE_ROWS, k, n)) for k in range(n)]
+            assert max(sizes) - min(sizes) <= STRIPE_ROWS  # balanced to within one stripe
