@@ -12,6 +12,10 @@
 
 #include "rtx.h"
 
+#ifndef RTX_PHILOX_CACHE
+#define RTX_PHILOX_CACHE 0
+#endif
+
 namespace rtxd {
 
 constexpr double kPi = 3.14159265358979323846;
@@ -60,7 +64,19 @@ __device__ __forceinline__ V3 refract(V3 uv, V3 n, double eta) {                
 // ---------------------------------------------------------------------------------------
 struct Rng {
   uint32_t k0, k1, pixel, sample, draw;
+#if RTX_PHILOX_CACHE
+  // one Philox block yields two doubles: keep the odd draw for the next call
+  double spare;
+  bool have_spare;
+#endif
   __device__ __forceinline__ double next() {
+#if RTX_PHILOX_CACHE
+    if ((draw & 1) && have_spare) {
+      have_spare = false;
+      draw++;
+      return spare;
+    }
+#endif
     uint32_t c0 = draw >> 1, c1 = sample, c2 = pixel, c3 = 0u;
     uint32_t a = k0, b = k1;
 #pragma unroll
@@ -75,6 +91,12 @@ struct Rng {
     }
     uint32_t lo = (draw & 1) ? c2 : c0;
     uint32_t hi = (draw & 1) ? c3 : c1;
+#if RTX_PHILOX_CACHE
+    if (!(draw & 1)) {
+      spare = (double)((((uint64_t)c3 << 32) | c2) >> 11) * 0x1p-53;
+      have_spare = true;
+    }
+#endif
     draw++;
     uint64_t bits = ((uint64_t)hi << 32) | lo;
     return (double)(bits >> 11) * 0x1p-53;
@@ -86,6 +108,9 @@ __device__ __forceinline__ Rng make_rng(uint64_t seed, uint32_t pixel, uint32_t 
   g.k0 = (uint32_t)seed;
   g.k1 = (uint32_t)(seed >> 32) ^ 0x52545831u;
   g.pixel = pixel, g.sample = sample, g.draw = draw;
+#if RTX_PHILOX_CACHE
+  g.spare = 0.0, g.have_spare = false;
+#endif
   return g;
 }
 

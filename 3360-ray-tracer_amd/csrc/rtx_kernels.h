@@ -22,7 +22,10 @@ namespace rtxd {
 constexpr int kBlock = 256;
 
 #ifndef RTX_TRACE_WAVES
-#define RTX_TRACE_WAVES 2  // min waves per SIMD requested for the trace kernels
+#define RTX_TRACE_WAVES 4  // min waves per SIMD for the trace kernels (<= 128 VGPRs; measured best)
+#endif
+#ifndef RTX_REFILL_MIN
+#define RTX_REFILL_MIN 32  // persistent lanes: refill once this many lanes of a wave are idle (A/B: 1/8/16/32)
 #endif
 
 // Pixel subset of the image handled by one call (rectangle or interleaved row stripes).
@@ -251,12 +254,15 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
   P.depth = 0, P.draw = 0;
   uint64_t slot = 0;
   int x = 0, y = 0, k = 0;
+  Rng g = make_rng(A.seed, 0u, 0u, 0u);  // the lane's path stream, kept across segments
   const unsigned long long lt = (1ull << lane_id()) - 1ull;
   while (true) {
-    // ---- refill: ballot of idle lanes, leftover of the current chunk first ----
+    // ---- refill: ballot of idle lanes, leftover of the current chunk first.  Refilling
+    // only once RTX_REFILL_MIN lanes are idle (or the wave is empty) amortises the
+    // primary-generation code over several lanes.
     const unsigned long long idle = __ballot(!has);
     bool fresh = false;
-    if (idle != 0 && !exhausted) {
+    if (idle != 0 && !exhausted && (__popcll(idle) >= RTX_REFILL_MIN || idle == ~0ull)) {
       const uint64_t nidle = (uint64_t)__popcll(idle);
       const uint64_t rank = (uint64_t)__popcll(idle & lt);
       if (chunk_left >= nidle) {
@@ -284,7 +290,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
       if (!(A.conv && A.conv[p])) {
         k = (int)(slot - (uint64_t)p * A.K);
         A.map.xy(p, x, y);
-        Rng g = make_rng(A.seed, (uint32_t)(y * A.map.W + x), (uint32_t)(A.s0 + k), 0u);
+        g = make_rng(A.seed, (uint32_t)(y * A.map.W + x), (uint32_t)(A.s0 + k), 0u);
         get_ray(A.cam, x, y, g, P.o, P.d);
         P.draw = g.draw;
         P.thr = v3(1.0, 1.0, 1.0);
@@ -307,7 +313,6 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
     } else {
       const int64_t best = trace<STACK, FAST, COUNT>(A.S, P.o, P.d, tmin, kInf, stk, c);
       segs++;
-      Rng g = make_rng(A.seed, (uint32_t)(y * A.map.W + x), (uint32_t)(A.s0 + k), P.draw);
       Hit h;
       if (best >= 0) finish_hit<false>(A.S, best, P.o, P.d, tmin, h);
       if (SCATTER) {

@@ -10,7 +10,7 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 REPO = os.path.dirname(PKG_DIR)
-LIB_PATH = os.path.join(PKG_DIR, "librtx.so")
+LIB_PATH = os.environ.get("RTX_LIB") or os.path.join(PKG_DIR, "librtx.so")  # RTX_LIB: A/B variant builds
 ASSETS = os.path.join(PKG_DIR, "assets")
 CAMERAS = os.path.join(REPO, "configs", "cameras.json")
 

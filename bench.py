@@ -54,6 +54,7 @@ def main():
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (=RCCL, one GPU per rank) or gloo (rehearsal)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -65,11 +66,13 @@ def main():
 
     dist = None
     torch.cuda.init()
-    torch.cuda.set_device(local if world > 1 else 0)
+    # one process per GPU; a gloo rehearsal may place several ranks on fewer devices
+    dev_id = local % max(1, torch.cuda.device_count()) if world > 1 else 0
+    torch.cuda.set_device(dev_id)
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl")
+        dist.init_process_group(args.dist_backend)
 
     import rtx
 
@@ -77,7 +80,7 @@ def main():
     spp = args.spp or spp
     total_spp = spp * world  # weak scaling: N x samples over 1/N of the pixels
     host = rtx.HostScene.recipe(scene_name, 1234)
-    dev = rtx.DeviceScene(host, device=local if world > 1 else 0)
+    dev = rtx.DeviceScene(host, device=dev_id)
     cam = rtx.camera(rtx.camera_config(preset, width=width))
     p = rtx.RenderParams()
     p.spp, p.max_depth, p.adaptive, p.seed = total_spp, depth, 0, args.seed
@@ -86,7 +89,6 @@ def main():
         p.stripe_rows, p.stripe_index, p.stripe_count = STRIPE_ROWS, rank, world
     npix = rtx.lib().rtx_render_pixel_count(cam, p)
 
-    dev_id = local if world > 1 else 0
     d_rgb = torch.empty((npix, 3), dtype=torch.float64, device=f"cuda:{dev_id}")
     d_spp = torch.empty((npix,), dtype=torch.int32, device=f"cuda:{dev_id}")
 
@@ -110,10 +112,11 @@ def main():
     hot_ms = sum(s["hot_kernel_ms"] for s in stats)
     hot_launches = sum(s["hot_launches"] for s in stats)
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{dev_id}")
+        red_dev = "cpu" if args.dist_backend == "gloo" else f"cuda:{dev_id}"
+        t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        r = torch.tensor([rays], dtype=torch.float64, device=f"cuda:{dev_id}")
+        r = torch.tensor([rays], dtype=torch.float64, device=red_dev)
         dist.all_reduce(r, op=dist.ReduceOp.SUM)
         rays_all = float(r.item())
     else:

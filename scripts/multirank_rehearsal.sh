@@ -1,0 +1,7 @@
+#!/bin/bash
+# bench.py's N>1 path on a single GPU: 2 ranks (gloo barrier/reductions) sharing cuda:0.
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
+mkdir -p gpurun_out
+timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29533 bench.py --gpus 2 --steps 2 --warmup 1 --dist-backend gloo "$@" \
+  > gpurun_out/bench_rehearsal_2rank.json 2> gpurun_out/bench_rehearsal_2rank.err
