@@ -23,10 +23,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     d, rnd, workload, mode, prec = sys.argv[1:6]
     tag = os.path.basename(d.rstrip("/")).replace("prof_", "")
-    prof = os.path.join(ROOT, "profiles")
+    prof = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(prof, exist_ok=True)
     stats = glob.glob(os.path.join(d, "trace", "*kernel_stats.csv"))[0]
-    shutil.copyfile(stats, os.path.join(prof, f"{rnd}_{tag}_kernel_stats.csv"))
+    shutil.copyfile(stats, os.path.join(prof, f"kernel_stats_{tag}.csv"))
+    bench = os.path.join(d, "bench_trace.json")
+    if os.path.exists(bench):
+        shutil.copyfile(bench, os.path.join(prof, f"bench_under_rocprof_{tag}.json"))
     counters = collections.defaultdict(lambda: collections.defaultdict(float))
     launches = collections.defaultdict(set)
     for f in glob.glob(os.path.join(d, "pmc_*", "*counter_collection.csv")):
@@ -38,7 +41,7 @@ def main():
     for k, v in counters.items():
         n = max(len(launches[(k, c)]) for c in v)
         out[k] = {"launches": n, **v}
-    json.dump(out, open(os.path.join(prof, f"{rnd}_{tag}_pmc.json"), "w"), indent=1, sort_keys=True)
+    json.dump(out, open(os.path.join(prof, f"pmc_{tag}.json"), "w"), indent=1, sort_keys=True)
     hot = "k_persistent<32, true, false, false>" if mode == "persistent" else "k_wf_extend<32, true, false>"
     if prec == "parity":
         hot = hot.replace("true, false", "false, false", 1)
@@ -49,8 +52,9 @@ def main():
             per = v["FETCH_SIZE"] * 2 * 1024 / n_f + v["WRITE_SIZE"] * 1024 / n_w
             t = {"kernel": k, "hbm_bytes_per_launch": per, "fetch_kib_total": v["FETCH_SIZE"],
                  "write_kib_total": v["WRITE_SIZE"], "launches_fetch_pass": n_f, "launches_write_pass": n_w,
-                 "source": f"profiles/{rnd}_{tag}_pmc.json", "correction": "FETCH_SIZE x2 (gfx950)"}
-            json.dump(t, open(os.path.join(prof, f"traffic_{workload}_{mode}_{prec}.json"), "w"), indent=1)
+                 "source": f"profiles/{rnd}/pmc_{tag}.json", "correction": "FETCH_SIZE x2 (gfx950)"}
+            json.dump(t, open(os.path.join(ROOT, "profiles", f"traffic_{workload}_{mode}_{prec}.json"), "w"),
+                      indent=1)
             print(json.dumps(t))
 
 
