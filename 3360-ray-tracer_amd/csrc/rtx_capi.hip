@@ -77,6 +77,7 @@ struct rtx_scene {
   std::vector<DevBuf> texels;
   DScene S{};
   int stack_parity = 32, stack_fast = 32;
+  bool fast_ok = false;  // RTX_PREC_FAST available (BVH with an internal root)
   int64_t n_nodes = 0;
   // render workspace (grow-only)
   DevBuf px_sum, px_mean, px_m2, px_samples, px_conv, lbuf, queue[2], counters, out_rgb, out_spp, rays, hits;
@@ -114,7 +115,7 @@ int bvh_depth(const rtx_bvh_node* n, int64_t count) {
 
 // BVH2 fast layout: one FNode per internal node, holding both children's outward-rounded
 // f32 boxes (see rtx_device.h FNode / fbox).
-void build_fast(const rtx_bvh_node* n, int64_t count, std::vector<FNode>& out) {
+[[maybe_unused]] void build_fast(const rtx_bvh_node* n, int64_t count, std::vector<FNode>& out) {
   std::vector<int32_t> fidx(count, -1);
   int32_t k = 0;
   for (int64_t i = 0; i < count; i++)
@@ -137,6 +138,71 @@ void build_fast(const rtx_bvh_node* n, int64_t count, std::vector<FNode>& out) {
       else f.c1 = ref, f.n1 = cnt;
     }
   }
+}
+
+// BVH4 fast layout: the binary tree collapsed top-down.  Each F4Node starts from the binary
+// node's two children and repeatedly opens the internal child with the largest surface area
+// (children stay in left-to-right order) until it holds four slots or only leaves remain.
+// Leaves are the binary leaves, unchanged; every slot keeps its binary node's box, rounded
+// outward.  Returns the exact worst-case traversal stack depth of the collapsed tree
+// (trace_fast4 pushes at most `internal slots - 1` entries per visited node), or -1 when a
+// leaf is too large for the 16-bit slot count.
+[[maybe_unused]] int build_fast4(const rtx_bvh_node* n, std::vector<F4Node>& out) {
+  out.clear();
+  auto area = [&](uint32_t i) {
+    const double dx = n[i].hi[0] - n[i].lo[0], dy = n[i].hi[1] - n[i].lo[1], dz = n[i].hi[2] - n[i].lo[2];
+    return dx * dy + dy * dz + dz * dx;
+  };
+  int need = 0;
+  bool ok = true;
+  // iterative pre-order: (binary node, F4 slot to patch, stack depth on arrival)
+  struct Item {
+    uint32_t bin;
+    int64_t parent_slot;
+    int depth;
+  };
+  std::vector<Item> work{{0u, -1, 0}};
+  while (!work.empty()) {
+    const Item it = work.back();
+    work.pop_back();
+    const int32_t me = (int32_t)out.size();
+    if (it.parent_slot >= 0) out[it.parent_slot >> 2].child[it.parent_slot & 3] = me;
+    out.push_back(F4Node{});
+    std::vector<uint32_t> slots{n[it.bin].left_first, n[it.bin].right_count};
+    while (slots.size() < 4) {
+      int pick = -1;
+      double best = -1.0;
+      for (size_t k = 0; k < slots.size(); k++)
+        if (!n[slots[k]].is_leaf && area(slots[k]) > best) best = area(slots[k]), pick = (int)k;
+      if (pick < 0) break;
+      const uint32_t b = slots[pick];
+      slots[pick] = n[b].left_first;
+      slots.insert(slots.begin() + pick + 1, n[b].right_count);
+    }
+    int internal = 0;
+    for (uint32_t b : slots) internal += n[b].is_leaf ? 0 : 1;
+    const int child_depth = it.depth + std::max(0, internal - 1);
+    need = std::max(need, child_depth);
+    F4Node& f = out[me];
+    for (int c = 0; c < 4; c++) {
+      if (c >= (int)slots.size()) {  // empty slot: empty leaf
+        f.child[c] = -1;
+        continue;
+      }
+      const rtx_bvh_node& cn = n[slots[c]];
+      f.lox[c] = round_down(cn.lo[0]), f.loy[c] = round_down(cn.lo[1]), f.loz[c] = round_down(cn.lo[2]);
+      f.hix[c] = round_up(cn.hi[0]), f.hiy[c] = round_up(cn.hi[1]), f.hiz[c] = round_up(cn.hi[2]);
+      if (cn.is_leaf) {
+        if (cn.right_count > 0xffffu) ok = false;
+        f.child[c] = ~(int32_t)cn.left_first;
+        f.counts[c >> 1] |= (cn.right_count & 0xffffu) << (16 * (c & 1));
+      }
+    }
+    // push in reverse so children are laid out in slot order (pre-order)
+    for (int c = (int)slots.size() - 1; c >= 0; c--)
+      if (!n[slots[c]].is_leaf) work.push_back({slots[c], (int64_t)me * 4 + c, child_depth});
+  }
+  return ok ? need : -1;
 }
 
 int pick_stack(int depth) {
@@ -329,14 +395,24 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   if ((rc = upload(sc->images, imgs.data(), imgs.size(), s))) return rc;
   sc->n_nodes = d->nodes ? d->n_nodes : 0;
   std::vector<FNode> fn;
+  std::vector<F4Node> f4;
   if (d->nodes && d->n_nodes > 0) {
     if ((rc = upload(sc->nodes, d->nodes, d->n_nodes, s))) return rc;
     const int depth = bvh_depth(d->nodes, d->n_nodes);
     sc->stack_parity = pick_stack(depth);
     sc->stack_fast = sc->stack_parity;
     if (sc->stack_parity < 0) return fail(RTX_ERR_INVALID, "BVH deeper than 62 levels");
-    build_fast(d->nodes, d->n_nodes, fn);
-    if ((rc = upload(sc->fnodes, fn.data(), fn.size(), s))) return rc;
+    if (!d->nodes[0].is_leaf) {
+#if RTX_BVH4
+      const int need = build_fast4(d->nodes, f4);
+      sc->stack_fast = need < 0 ? -1 : (need <= 32 ? 32 : (need <= 64 ? 64 : -1));
+      if (sc->stack_fast > 0 && (rc = upload(sc->fnodes, f4.data(), f4.size(), s))) return rc;
+#else
+      build_fast(d->nodes, d->n_nodes, fn);
+      if ((rc = upload(sc->fnodes, fn.data(), fn.size(), s))) return rc;
+#endif
+      sc->fast_ok = sc->stack_fast > 0;
+    }
   }
   HIPC(hipStreamSynchronize(s));
   DScene& S = sc->S;
@@ -346,6 +422,7 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   S.texs = sc->texs.as<rtx_texture>();
   S.images = sc->images.as<DImage>();
   S.fnodes = fn.empty() ? nullptr : sc->fnodes.as<FNode>();
+  S.f4nodes = (f4.empty() || !sc->fast_ok) ? nullptr : sc->fnodes.as<F4Node>();
   S.use_bvh = (d->nodes && d->n_nodes > 0) ? 1 : 0;
   S.n_prims = S.use_bvh ? d->n_prims : d->n_prims;
   S.froot_leaf = 0, S.froot_count = 0;
@@ -367,7 +444,7 @@ int rtx_intersect_device(rtx_scene* sc, const rtx_ray* d_rays, size_t n, rtx_hit
   if (!d_rays || !d_hits) return fail(RTX_ERR_INVALID, "NULL buffer");
   HIPC(hipSetDevice(sc->device));
   hipStream_t s = stream ? (hipStream_t)stream : sc->stream;
-  const bool fast = precision == RTX_PREC_FAST && sc->S.fnodes;
+  const bool fast = precision == RTX_PREC_FAST && sc->fast_ok;
   const int st = fast ? sc->stack_fast : sc->stack_parity;
   if (fast) return st == 32 ? launch_intersect<32, true>(sc, d_rays, (int64_t)n, d_hits, tmin, tmax, s)
                             : launch_intersect<64, true>(sc, d_rays, (int64_t)n, d_hits, tmin, tmax, s);
@@ -467,7 +544,7 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
   if (npix < 0) return fail(RTX_ERR_INVALID, err);
   HIPC(hipSetDevice(sc->device));
   hipStream_t s = stream ? (hipStream_t)stream : sc->stream;
-  const bool fast = prm->precision == RTX_PREC_FAST && sc->S.fnodes;
+  const bool fast = prm->precision == RTX_PREC_FAST && sc->fast_ok;
   Launch L{sc, s, fast ? sc->stack_fast : sc->stack_parity, fast, (prm->flags & RTX_FLAG_COUNT) != 0};
 
   // samples in flight per pixel (group size K)
@@ -616,6 +693,7 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
     stats->hot_launches = hot_launches;
     stats->node_visits = h[2];
     stats->prim_tests = h[3];
+    stats->node_bytes = (L.fast && RTX_BVH4) ? sizeof(F4Node) : (L.fast ? sizeof(FNode) : sizeof(rtx_bvh_node));
   }
   return RTX_OK;
 }

@@ -169,6 +169,19 @@ struct FNode {
 };
 static_assert(sizeof(FNode) == 64, "FNode must be one 64-byte line");
 
+// 4-wide fast node (RTX_PREC_FAST with RTX_BVH4): the reference's binary SAH tree collapsed
+// so every node holds up to four children's outward-rounded f32 boxes (SoA for the four
+// slab tests).  Leaves are the binary tree's leaves, unchanged.  child >= 0: node index;
+// child < 0: leaf, ~child = first prim, count in 16-bit half (c & 1) of counts[c >> 1];
+// empty slot: an empty leaf (child -1, count 0).  128 bytes = two cache lines.
+struct F4Node {
+  float lox[4], loy[4], loz[4], hix[4], hiy[4], hiz[4];
+  int32_t child[4];
+  uint32_t counts[2];
+  uint32_t pad_[2];
+};
+static_assert(sizeof(F4Node) == 128, "F4Node must be two 64-byte lines");
+
 struct DScene {
   const rtx_bvh_node* nodes;  // parity layout, reference pre-order
   const rtx_prim* prims;      // leaf order
@@ -176,6 +189,7 @@ struct DScene {
   const rtx_texture* texs;
   const DImage* images;
   const FNode* fnodes;  // fast layout (root at 0) or nullptr
+  const F4Node* f4nodes;  // 4-wide fast layout (root at 0) or nullptr
   int64_t n_prims;
   int32_t use_bvh;
   int32_t froot_leaf;  // fast BVH: the whole tree is one leaf (count in froot_count)
@@ -535,6 +549,95 @@ __device__ __forceinline__ int64_t trace_fast(const DScene& S, V3 o, V3 d, doubl
     } else {
       // pop, re-testing the popped node's box against the shrunk interval is implicit:
       // its box was tested when pushed; a stale far child is re-culled at its own node.
+      if (sp == 0) break;
+      node = (int32_t)stk[(--sp) * stride];
+    }
+  }
+  return best;
+}
+
+// 4-wide fast traversal over F4Node (same conservative f32 slab test as trace_fast).  The
+// collapsed tree has exactly the binary tree's leaves, and every binary box that the f64
+// test accepts is still accepted (each F4Node slot carries the outward-rounded box of the
+// binary node it replaces), so the candidate primitive set again contains the reference's
+// and the closest hit is the same.  Per node: the four slab tests, leaves tested at once
+// (slot order), then the surviving internal children sorted by entry distance; the nearest
+// is visited next, the others are pushed far-to-near.  The host sizes STACK from the exact
+// worst-case push depth of the collapsed tree (rtx_capi.hip build_fast4).
+__device__ __forceinline__ void cswap4(float& ta, int32_t& ca, float& tb, int32_t& cb) {
+  const bool s = tb < ta;
+  const float t = s ? tb : ta;
+  tb = s ? ta : tb;
+  ta = t;
+  const int32_t c = s ? cb : ca;
+  cb = s ? ca : cb;
+  ca = c;
+}
+
+template <int STACK, bool COUNT>
+__device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
+                                               int stride, Counters& cnt) {
+  int64_t best = -1;
+  double closest = tmax, t;
+  if (!S.use_bvh || S.froot_leaf) {
+    const int64_t n = S.use_bvh ? S.froot_count : S.n_prims;
+    for (int64_t i = 0; i < n; i++) {
+      if (COUNT) cnt.prims++;
+      if (prim_t(S.prims + i, o, d, tmin, closest, t)) closest = t, best = i;
+    }
+    return best;
+  }
+  const FRay r = make_fray(o, d);
+  float tmax_f = f32_round_up(closest);
+  int sp = 0;
+  int32_t node = 0;
+  while (true) {
+    const F4Node* __restrict__ nd = S.f4nodes + node;
+    if (COUNT) cnt.nodes++;
+    float tt[4];
+    int32_t cc[4];
+    const uint32_t counts01 = nd->counts[0], counts23 = nd->counts[1];
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const float lo[3] = {nd->lox[c], nd->loy[c], nd->loz[c]};
+      const float hi[3] = {nd->hix[c], nd->hiy[c], nd->hiz[c]};
+      tt[c] = fbox(lo, hi, r, 0.0f, tmax_f);
+      cc[c] = nd->child[c];
+    }
+    bool shrink = false;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      if (tt[c] != __builtin_inff() && cc[c] < 0) {
+        const uint32_t first = (uint32_t)(~cc[c]);
+        const uint32_t n = ((c < 2 ? counts01 : counts23) >> (16 * (c & 1))) & 0xffffu;
+        for (uint32_t i = 0; i < n; i++) {
+          if (COUNT) cnt.prims++;
+          if (prim_t(S.prims + first + i, o, d, tmin, closest, t)) closest = t, best = (int64_t)first + i, shrink = true;
+        }
+        tt[c] = __builtin_inff();
+      }
+    }
+    if (shrink) {
+      tmax_f = f32_round_up(closest);
+#pragma unroll
+      for (int c = 0; c < 4; c++)
+        if (tt[c] > tmax_f) tt[c] = __builtin_inff();
+    }
+    cswap4(tt[0], cc[0], tt[1], cc[1]);
+    cswap4(tt[2], cc[2], tt[3], cc[3]);
+    cswap4(tt[0], cc[0], tt[2], cc[2]);
+    cswap4(tt[1], cc[1], tt[3], cc[3]);
+    cswap4(tt[1], cc[1], tt[2], cc[2]);
+    if (tt[0] != __builtin_inff()) {
+#pragma unroll
+      for (int c = 3; c >= 1; c--) {
+        if (tt[c] != __builtin_inff()) {
+          if (sp + 1 > STACK) __builtin_trap();
+          stk[(sp++) * stride] = (uint32_t)cc[c];
+        }
+      }
+      node = cc[0];
+    } else {
       if (sp == 0) break;
       node = (int32_t)stk[(--sp) * stride];
     }

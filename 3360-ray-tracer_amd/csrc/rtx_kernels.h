@@ -24,6 +24,9 @@ constexpr int kBlock = 256;
 #ifndef RTX_TRACE_WAVES
 #define RTX_TRACE_WAVES 4  // min waves per SIMD for the trace kernels (<= 128 VGPRs; measured best)
 #endif
+#ifndef RTX_BVH4
+#define RTX_BVH4 1  // fast precision traverses the 4-wide collapse of the SAH tree (else BVH2)
+#endif
 #ifndef RTX_REFILL_MIN
 #define RTX_REFILL_MIN 32  // persistent lanes: refill once this many lanes of a wave are idle (A/B: 1/8/16/32)
 #endif
@@ -88,7 +91,11 @@ __device__ __forceinline__ int64_t wave_compact(bool want, unsigned int* counter
 template <int STACK, bool FAST, bool COUNT>
 __device__ __forceinline__ int64_t trace(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
                                          Counters& c) {
+#if RTX_BVH4
+  if (FAST) return trace_fast4<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c);
+#else
   if (FAST) return trace_fast<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c);
+#endif
   return trace_parity<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c);
 }
 

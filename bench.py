@@ -129,7 +129,7 @@ def main():
     segs = max(1, cst["rays_total"])
     nodes_per_seg = cst["node_visits"] / segs
     prims_per_seg = cst["prim_tests"] / segs
-    node_bytes = 64  # fast: FNode (2 f32 child boxes); parity: rtx_bvh_node (f64 box) — both 64 B
+    node_bytes = cst["node_bytes"]  # fast: F4Node 128 B (4 f32 child boxes); parity: rtx_bvh_node 64 B
     prim_bytes = 80  # rtx_prim (f64 geometry + kind/material)
     state_bytes = 48 if args.mode == "persistent" else 48 + 88 + 88  # material 48 (+ SoA path state in/out)
     bytes_per_seg = node_bytes * nodes_per_seg + prim_bytes * prims_per_seg + state_bytes

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 1
+#define RTX_ABI_VERSION 2  /* 2: rtx_stats.node_bytes */
 
 enum {
   RTX_OK = 0,
@@ -203,6 +203,7 @@ typedef struct {
   uint64_t hot_launches;
   uint64_t node_visits;    /* with RTX_FLAG_COUNT */
   uint64_t prim_tests;     /* with RTX_FLAG_COUNT */
+  uint64_t node_bytes;     /* bytes of one BVH node visit in the traversal used (64 BVH2, 128 BVH4) */
 } rtx_stats;
 
 /* ---- entry points ------------------------------------------------------------------ */
