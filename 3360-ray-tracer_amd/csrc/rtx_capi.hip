@@ -225,6 +225,10 @@ int64_t subset_pixels(const rtx_camera* cam, const rtx_render_params* p, PixelMa
     err = "camera not initialised (image size <= 0)";
     return -1;
   }
+  if ((int64_t)m.W * m.H > 0x7FFFFFFFll) {  // pixel indices are 32-bit on the device
+    err = "image larger than 2^31 pixels";
+    return -1;
+  }
   if (p->stripe_rows > 0) {
     if (p->stripe_count <= 0 || p->stripe_index < 0 || p->stripe_index >= p->stripe_count) {
       err = "bad stripe_index/stripe_count";

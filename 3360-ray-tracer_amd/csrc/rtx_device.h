@@ -12,8 +12,12 @@
 
 #include "rtx.h"
 
-#ifndef RTX_PHILOX_CACHE
-#define RTX_PHILOX_CACHE 0
+// timing experiments only (tests fail with these): upper bounds of the RNG / trig cost
+#ifndef RTX_X_PHILOX_ROUNDS
+#define RTX_X_PHILOX_ROUNDS 10
+#endif
+#ifndef RTX_PHILOX_MAD
+#define RTX_PHILOX_MAD 1  // A/B r01: +2.3% C2, neutral bunny
 #endif
 
 namespace rtxd {
@@ -57,60 +61,68 @@ __device__ __forceinline__ V3 refract(V3 uv, V3 n, double eta) {                
 }
 
 // ---------------------------------------------------------------------------------------
-// Counter-based RNG: Philox-4x32-10, key (seed), counter (draw>>1, sample, pixel, 0).
-// Bit-identical to oracle/rtx_oracle.cc Rng::next (philox mode).  A path's stream depends
-// only on (seed, global pixel, sample), so results are independent of tiling, GPU count,
-// queue order and scheduling.
+// Counter-based RNG: Philox-4x32-10, key (seed_lo, seed_hi ^ 0x52545831), counter
+// (draw >> 1, sample, global pixel, stream).  Stream 0 is the camera ray (GetRay); the
+// shading of path segment n (n = 0 for the primary hit) is stream n + 1, and `draw`
+// restarts at 0 in every stream.  Draw 2k of a stream is words 0/1 of block k, draw 2k+1
+// words 2/3, as a 53-bit double.  Bit-identical to oracle/rtx_oracle.cc Rng::next (philox
+// mode).  A path's numbers depend only on (seed, pixel, sample, segment, draw): results
+// are independent of tiling, GPU count, queue order and scheduling.
+//
+// Because every stream starts block-aligned, the first block of a stream is computed once
+// in converged control flow (make_rng) and serves the first two draws of every material
+// branch; a later block is computed where the wave first needs it, with per-lane counters,
+// so lanes at different draw positions still share one Philox evaluation.
 // ---------------------------------------------------------------------------------------
-struct Rng {
-  uint32_t k0, k1, pixel, sample, draw;
-#if RTX_PHILOX_CACHE
-  // one Philox block yields two doubles: keep the odd draw for the next call
-  double spare;
-  bool have_spare;
-#endif
-  __device__ __forceinline__ double next() {
-#if RTX_PHILOX_CACHE
-    if ((draw & 1) && have_spare) {
-      have_spare = false;
-      draw++;
-      return spare;
-    }
-#endif
-    uint32_t c0 = draw >> 1, c1 = sample, c2 = pixel, c3 = 0u;
-    uint32_t a = k0, b = k1;
+__device__ __forceinline__ void philox_block(uint32_t blk, uint32_t sample, uint32_t pixel, uint32_t stream,
+                                             uint32_t k0, uint32_t k1, double& u0, double& u1) {
+  uint32_t c0 = blk, c1 = sample, c2 = pixel, c3 = stream;
+  uint32_t a = k0, b = k1;
 #pragma unroll
-    for (int r = 0; r < 10; r++) {
-      uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-      uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-      uint32_t n0 = hi1 ^ c1 ^ a;
-      uint32_t n2 = hi0 ^ c3 ^ b;
-      c0 = n0, c1 = lo1, c2 = n2, c3 = lo0;
-      a += 0x9E3779B9u;
-      b += 0xBB67AE85u;
-    }
-    uint32_t lo = (draw & 1) ? c2 : c0;
-    uint32_t hi = (draw & 1) ? c3 : c1;
-#if RTX_PHILOX_CACHE
-    if (!(draw & 1)) {
-      spare = (double)((((uint64_t)c3 << 32) | c2) >> 11) * 0x1p-53;
-      have_spare = true;
-    }
+  for (int r = 0; r < RTX_X_PHILOX_ROUNDS; r++) {
+#if RTX_PHILOX_MAD
+    // one v_mad_u64_u32 per product instead of v_mul_lo_u32 + v_mul_hi_u32
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
+    uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
+#else
+    uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
 #endif
+    uint32_t n0 = hi1 ^ c1 ^ a;
+    uint32_t n2 = hi0 ^ c3 ^ b;
+    c0 = n0, c1 = lo1, c2 = n2, c3 = lo0;
+    a += 0x9E3779B9u;
+    b += 0xBB67AE85u;
+  }
+  u0 = (double)((((uint64_t)c1 << 32) | c0) >> 11) * 0x1p-53;
+  u1 = (double)((((uint64_t)c3 << 32) | c2) >> 11) * 0x1p-53;
+}
+
+struct Rng {
+  uint32_t k0, k1, pixel, sample, stream, draw;
+  uint32_t cblk;   // block held in (ca, cb)
+  double ca, cb;   // draws 2*cblk, 2*cblk + 1
+  __device__ __forceinline__ double next() {
+    const uint32_t blk = draw >> 1;
+    if (blk != cblk) {
+      philox_block(blk, sample, pixel, stream, k0, k1, ca, cb);
+      cblk = blk;
+    }
+    const double r = (draw & 1) ? cb : ca;
     draw++;
-    uint64_t bits = ((uint64_t)hi << 32) | lo;
-    return (double)(bits >> 11) * 0x1p-53;
+    return r;
   }
   __device__ __forceinline__ double next(double mn, double mx) { return mn + (mx - mn) * next(); }
 };
-__device__ __forceinline__ Rng make_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t draw) {
+// Opens `stream` of (pixel, sample) at draw 0 with its first block already computed.
+__device__ __forceinline__ Rng make_rng(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t stream) {
   Rng g;
   g.k0 = (uint32_t)seed;
   g.k1 = (uint32_t)(seed >> 32) ^ 0x52545831u;
-  g.pixel = pixel, g.sample = sample, g.draw = draw;
-#if RTX_PHILOX_CACHE
-  g.spare = 0.0, g.have_spare = false;
-#endif
+  g.pixel = pixel, g.sample = sample, g.stream = stream, g.draw = 0;
+  philox_block(0u, sample, pixel, stream, g.k0, g.k1, g.ca, g.cb);
+  g.cblk = 0;
   return g;
 }
 
@@ -138,8 +150,13 @@ __device__ __forceinline__ V3 random_cosine_direction(Rng& g, V3 normal) {  // m
   double r2 = g.next();
   double phi = 2.0 * kPi * r1;
   double r = sqrt(r2);
+#if RTX_X_F32TRIG
+  double x = r * (double)cosf((float)phi);
+  double y = r * (double)sinf((float)phi);
+#else
   double x = r * cos(phi);
   double y = r * sin(phi);
+#endif
   double z = sqrt(1.0 - r2);
   V3 w = normalize(normal);
   V3 a = (fabs(w.x) > 0.9) ? v3(0, 1, 0) : v3(1, 0, 0);
@@ -556,14 +573,60 @@ __device__ __forceinline__ int64_t trace_fast(const DScene& S, V3 o, V3 d, doubl
   return best;
 }
 
-// 4-wide fast traversal over F4Node (same conservative f32 slab test as trace_fast).  The
-// collapsed tree has exactly the binary tree's leaves, and every binary box that the f64
-// test accepts is still accepted (each F4Node slot carries the outward-rounded box of the
-// binary node it replaces), so the candidate primitive set again contains the reference's
-// and the closest hit is the same.  Per node: the four slab tests, leaves tested at once
-// (slot order), then the surviving internal children sorted by entry distance; the nearest
-// is visited next, the others are pushed far-to-near.  The host sizes STACK from the exact
-// worst-case push depth of the collapsed tree (rtx_capi.hip build_fast4).
+// 4-wide fast traversal over F4Node.  The collapsed tree has exactly the binary tree's
+// leaves, and every binary box that the f64 test accepts is still accepted (each F4Node slot
+// carries the outward-rounded box of the binary node it replaces, and the slab test below is
+// conservative), so the candidate primitive set contains the reference's and the closest
+// hit is the same up to exact t ties.  Per node: four slab tests, the hit leaves' primitives
+// in one flattened loop (lanes stay converged whichever slots they hit), then the surviving
+// internal children sorted by entry distance; the nearest is visited next, the others are
+// pushed far-to-near.  The host sizes STACK from the exact worst-case push depth of the
+// collapsed tree (rtx_capi.hip build_fast4).
+//
+// Slab test, one FMA per plane: t = fma(plane, inv, n) with n = -(o * inv) -/+ delta.
+// With inv = RN(1/RN(d)), o_f = RN(o), n0 = RN(-o_f * inv), the computed plane distance is
+//   t_c = T (1 + e_rel) + E,  |e_rel| <= 2^-23 + 2^-24,  |E| <= |o * inv| * 2^-23 * (1 + 2^-20)
+// against the exact T = (plane - o) / d.  E is absorbed by shifting n outward by
+// delta = |n0| * 2^-20 (the entry plane's offset down, the exit plane's up, by the sign of
+// inv), e_rel by the 1e-5 relative slack on the entry/exit distances.  An axis whose offset
+// is not finite (inv = inf for a zero f32 component) is neutralised: inv = 0, n = -/+inf,
+// i.e. the slab imposes no constraint — a widening, hence still conservative.
+struct FRay4 {
+  float ix, iy, iz, nlx, nhx, nly, nhy, nlz, nhz;
+};
+__device__ __forceinline__ void fray4_axis(double o, double d, float& inv, float& nl, float& nh) {
+  inv = 1.0f / (float)d;
+  const float n0 = -((float)o * inv);
+  if (!(fabsf(n0) < __builtin_inff())) {
+    inv = 0.0f, nl = -__builtin_inff(), nh = __builtin_inff();
+    return;
+  }
+  const float delta = fabsf(n0) * 0x1p-20f;
+  // plane `lo` enters when inv >= 0 (offset down), exits when inv < 0 (offset up)
+  nl = inv >= 0.0f ? n0 - delta : n0 + delta;
+  nh = inv >= 0.0f ? n0 + delta : n0 - delta;
+}
+__device__ __forceinline__ FRay4 make_fray4(V3 o, V3 d) {
+  FRay4 r;
+  fray4_axis(o.x, d.x, r.ix, r.nlx, r.nhx);
+  fray4_axis(o.y, d.y, r.iy, r.nly, r.nhy);
+  fray4_axis(o.z, d.z, r.iz, r.nlz, r.nhz);
+  return r;
+}
+// entry distance (slack-widened) or +inf on a miss; NaN plane distances drop out of the
+// min/max (v_min/v_max_f32 return the non-NaN operand), which only widens the interval
+__device__ __forceinline__ float fbox4(float lx, float ly, float lz, float hx, float hy, float hz, const FRay4& r,
+                                       float tmax_f) {
+  const float tx0 = fmaf(lx, r.ix, r.nlx), tx1 = fmaf(hx, r.ix, r.nhx);
+  const float ty0 = fmaf(ly, r.iy, r.nly), ty1 = fmaf(hy, r.iy, r.nhy);
+  const float tz0 = fmaf(lz, r.iz, r.nlz), tz1 = fmaf(hz, r.iz, r.nhz);
+  float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
+  float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax_f));
+  tn = tn * 0.99999f;  // tn >= 0
+  tf = tf * 1.00001f;  // only tf >= tn >= 0 can pass
+  return tn <= tf ? tn : __builtin_inff();
+}
+
 __device__ __forceinline__ void cswap4(float& ta, int32_t& ca, float& tb, int32_t& cb) {
   const bool s = tb < ta;
   const float t = s ? tb : ta;
@@ -587,7 +650,7 @@ __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, doub
     }
     return best;
   }
-  const FRay r = make_fray(o, d);
+  const FRay4 r = make_fray4(o, d);
   float tmax_f = f32_round_up(closest);
   int sp = 0;
   int32_t node = 0;
@@ -599,29 +662,40 @@ __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, doub
     const uint32_t counts01 = nd->counts[0], counts23 = nd->counts[1];
 #pragma unroll
     for (int c = 0; c < 4; c++) {
-      const float lo[3] = {nd->lox[c], nd->loy[c], nd->loz[c]};
-      const float hi[3] = {nd->hix[c], nd->hiy[c], nd->hiz[c]};
-      tt[c] = fbox(lo, hi, r, 0.0f, tmax_f);
+      tt[c] = fbox4(nd->lox[c], nd->loy[c], nd->loz[c], nd->hix[c], nd->hiy[c], nd->hiz[c], r, tmax_f);
       cc[c] = nd->child[c];
     }
-    bool shrink = false;
+    // hit leaves (non-empty) -> mask; they leave the internal-child ordering
+    uint32_t lmask = 0;
 #pragma unroll
     for (int c = 0; c < 4; c++) {
-      if (tt[c] != __builtin_inff() && cc[c] < 0) {
-        const uint32_t first = (uint32_t)(~cc[c]);
-        const uint32_t n = ((c < 2 ? counts01 : counts23) >> (16 * (c & 1))) & 0xffffu;
-        for (uint32_t i = 0; i < n; i++) {
-          if (COUNT) cnt.prims++;
-          if (prim_t(S.prims + first + i, o, d, tmin, closest, t)) closest = t, best = (int64_t)first + i, shrink = true;
-        }
+      const uint32_t n = ((c < 2 ? counts01 : counts23) >> (16 * (c & 1))) & 0xffffu;
+      if (cc[c] < 0) {
+        if (tt[c] != __builtin_inff() && n != 0) lmask |= 1u << c;
         tt[c] = __builtin_inff();
       }
     }
-    if (shrink) {
-      tmax_f = f32_round_up(closest);
+    if (lmask) {
+      bool shrink = false;
+      uint32_t cur = 0, left = 0;
+      while (lmask | left) {
+        if (left == 0) {
+          const int c = __builtin_ctz(lmask);
+          lmask &= lmask - 1u;
+          const int32_t ch = c == 0 ? cc[0] : (c == 1 ? cc[1] : (c == 2 ? cc[2] : cc[3]));
+          cur = (uint32_t)(~ch);
+          left = ((c < 2 ? counts01 : counts23) >> (16 * (c & 1))) & 0xffffu;
+        }
+        if (COUNT) cnt.prims++;
+        if (prim_t(S.prims + cur, o, d, tmin, closest, t)) closest = t, best = (int64_t)cur, shrink = true;
+        cur++, left--;
+      }
+      if (shrink) {
+        tmax_f = f32_round_up(closest);
 #pragma unroll
-      for (int c = 0; c < 4; c++)
-        if (tt[c] > tmax_f) tt[c] = __builtin_inff();
+        for (int c = 0; c < 4; c++)
+          if (tt[c] > tmax_f) tt[c] = __builtin_inff();
+      }
     }
     cswap4(tt[0], cc[0], tt[1], cc[1]);
     cswap4(tt[2], cc[2], tt[3], cc[3]);
@@ -818,11 +892,11 @@ __device__ __forceinline__ void get_ray(const rtx_camera& c, int i, int j, Rng& 
   d = ps - o;
 }
 
-// Path state between bounces (RayState, ray_state.h:8-13) + RNG draw counter.
+// Path state between bounces (RayState, ray_state.h:8-13).  The RNG needs no state of its
+// own: segment `depth` shades with stream depth + 1 (see Rng).
 struct Path {
   V3 o, d, thr;
   int32_t depth;
-  uint32_t draw;
 };
 
 // One shading step (wavefront.cc:109-208).  true: continue with p updated; false: path
@@ -859,7 +933,6 @@ __device__ __forceinline__ bool shade(const DScene& S, int max_depth, Path& p, c
     if (g.next() > q) return false;
     c.thr = c.thr / q;
   }
-  c.draw = g.draw;
   p = c;
   return true;
 }

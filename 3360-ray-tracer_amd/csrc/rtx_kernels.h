@@ -37,13 +37,15 @@ struct PixelMap {
   int32_t stripes;  // 0: rectangle, 1: stripes
   int32_t x0, y0, w, h;
   int32_t srows, sidx, scount;
-  __device__ __forceinline__ void xy(int64_t local, int& x, int& y) const {
+  // 32-bit arithmetic: the host keeps pixel counts below 2^31
+  __device__ __forceinline__ void xy(uint32_t local, int& x, int& y) const {
     if (!stripes) {
-      x = x0 + (int)(local % w);
-      y = y0 + (int)(local / w);
+      const uint32_t r = local / (uint32_t)w;
+      x = x0 + (int)(local - r * (uint32_t)w);
+      y = y0 + (int)r;
     } else {
-      int r = (int)(local / W);
-      x = (int)(local % W);
+      const int r = (int)(local / (uint32_t)W);
+      x = (int)(local - (uint32_t)r * (uint32_t)W);
       int blk = r / srows;
       y = (blk * scount + sidx) * srows + r % srows;
     }
@@ -53,7 +55,7 @@ struct PixelMap {
 struct PathQueue {  // SoA, one entry per in-flight path
   double *ox, *oy, *oz, *dx, *dy, *dz, *tx, *ty, *tz;
   uint32_t* slot;
-  uint32_t* meta;  // depth << 24 | draw
+  uint32_t* meta;  // path depth (segment index); the RNG stream is depth + 1
   int32_t* hit;    // closest primitive (leaf order) or -1, written by k_wf_extend
 };
 
@@ -161,7 +163,6 @@ __global__ __launch_bounds__(kBlock) void k_wf_generate(RenderArgs A, PathQueue 
       A.map.xy(p, x, y);
       Rng g = make_rng(A.seed, (uint32_t)(y * A.map.W + x), (uint32_t)(A.s0 + k), 0u);
       get_ray(A.cam, x, y, g, P.o, P.d);
-      P.draw = g.draw;
       made++;
     }
     const int64_t dst = wave_compact(live, count);
@@ -170,7 +171,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_generate(RenderArgs A, PathQueue 
       q.dx[dst] = P.d.x, q.dy[dst] = P.d.y, q.dz[dst] = P.d.z;
       q.tx[dst] = 1.0, q.ty[dst] = 1.0, q.tz[dst] = 1.0;
       q.slot[dst] = (uint32_t)slot;
-      q.meta[dst] = P.draw;  // depth 0
+      q.meta[dst] = 0u;  // depth 0
     }
   }
   flush_counters(A, Counters{0, 0}, 0, made, false);
@@ -209,8 +210,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in,
       P.thr = v3(in.tx[i], in.ty[i], in.tz[i]);
       slot = in.slot[i];
       const uint32_t meta = in.meta[i];
-      P.depth = (int32_t)(meta >> 24);
-      P.draw = meta & 0xFFFFFFu;
+      P.depth = (int32_t)meta;
       const int64_t p = slot / A.K;
       const int k = (int)(slot - p * A.K);
       int x, y;
@@ -218,7 +218,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in,
       const int32_t best = in.hit[i];
       Hit h;
       if (best >= 0) finish_hit<false>(A.S, best, P.o, P.d, (double)0.001f, h);
-      Rng g = make_rng(A.seed, (uint32_t)(y * A.map.W + x), (uint32_t)(A.s0 + k), P.draw);
+      Rng g = make_rng(A.seed, (uint32_t)(y * A.map.W + x), (uint32_t)(A.s0 + k), (uint32_t)P.depth + 1u);
       V3 L;
       cont = shade(A.S, A.max_depth, P, h, best >= 0, g, L);
       if (!cont) {
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in,
       out.dx[dst] = P.d.x, out.dy[dst] = P.d.y, out.dz[dst] = P.d.z;
       out.tx[dst] = P.thr.x, out.ty[dst] = P.thr.y, out.tz[dst] = P.thr.z;
       out.slot[dst] = slot;
-      out.meta[dst] = ((uint32_t)P.depth << 24) | (P.draw & 0xFFFFFFu);
+      out.meta[dst] = (uint32_t)P.depth;
     }
   }
 }
@@ -258,10 +258,9 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
   bool exhausted = false;                   // wave-uniform
   bool has = false;
   Path P;
-  P.depth = 0, P.draw = 0;
+  P.depth = 0;
   uint64_t slot = 0;
-  int x = 0, y = 0, k = 0;
-  Rng g = make_rng(A.seed, 0u, 0u, 0u);  // the lane's path stream, kept across segments
+  uint32_t pix = 0, smp = 0;  // RNG identity of the lane's path: global pixel, sample
   const unsigned long long lt = (1ull << lane_id()) - 1ull;
   while (true) {
     // ---- refill: ballot of idle lanes, leftover of the current chunk first.  Refilling
@@ -293,13 +292,15 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
     }
     // ---- start the primary path of a freshly assigned slot ----
     if (fresh && slot < nslots) {
-      const int64_t p = (int64_t)(slot / (uint64_t)A.K);
+      // nslots < 2^32 (checked on the host): 32-bit division
+      const uint32_t p = (uint32_t)slot / (uint32_t)A.K;
       if (!(A.conv && A.conv[p])) {
-        k = (int)(slot - (uint64_t)p * A.K);
+        const int k = (int)((uint32_t)slot - p * (uint32_t)A.K);
+        int x, y;
         A.map.xy(p, x, y);
-        g = make_rng(A.seed, (uint32_t)(y * A.map.W + x), (uint32_t)(A.s0 + k), 0u);
+        pix = (uint32_t)(y * A.map.W + x), smp = (uint32_t)(A.s0 + k);
+        Rng g = make_rng(A.seed, pix, smp, 0u);
         get_ray(A.cam, x, y, g, P.o, P.d);
-        P.draw = g.draw;
         P.thr = v3(1.0, 1.0, 1.0);
         P.depth = SCATTER ? A.max_depth : 0;
         has = true;
@@ -320,8 +321,18 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
     } else {
       const int64_t best = trace<STACK, FAST, COUNT>(A.S, P.o, P.d, tmin, kInf, stk, c);
       segs++;
+#if RTX_X_DUP_TRACE  // timing experiment: marginal cost of one more traversal
+      {
+        V3 od = P.d;
+        asm volatile("" : "+v"(od.x));
+        const int64_t b2 = trace<STACK, FAST, COUNT>(A.S, P.o, od, tmin, kInf, stk, c);
+        if (b2 == -7) A.counters[7] = 1;
+      }
+#endif
       Hit h;
       if (best >= 0) finish_hit<false>(A.S, best, P.o, P.d, tmin, h);
+      // stream of this segment: depth + 1 (GetPixel: depth counts down from max_depth)
+      Rng g = make_rng(A.seed, pix, smp, SCATTER ? (uint32_t)(A.max_depth - P.depth) + 1u : (uint32_t)P.depth + 1u);
       if (SCATTER) {
         // GetPixel(r, depth) iteratively (camera.h:148-174); P.thr holds the product of the
         // attenuations, P.depth the remaining depth.  Emitters never scatter, so the
@@ -336,7 +347,6 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
             P.thr = P.thr * att;
             P.o = h.p, P.d = sd;
             P.depth--;
-            P.draw = g.draw;
             cont = true;
           } else {
             L = P.thr * mat_emitted(A.S, m, h);
@@ -344,6 +354,25 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
           }
         }
       } else {
+#if RTX_X_DUP_SHADE  // timing experiment: marginal cost of one more shading step
+        {
+          Path P2 = P;
+          asm volatile("" : "+v"(P2.d.x));
+          Rng g2 = g;
+          V3 L2;
+          const bool c2 = shade(A.S, A.max_depth, P2, h, best >= 0, g2, L2);
+          if (c2 && L2.x == -7.0 && P2.d.y == -7.0) A.counters[7] = 1;
+        }
+#endif
+#if RTX_X_DUP_RNG  // timing experiment: marginal cost of one more Philox block
+        {
+          uint32_t s2 = smp;
+          asm volatile("" : "+v"(s2));
+          double u0, u1;
+          philox_block(1u, s2, pix, (uint32_t)P.depth + 1u, g.k0, g.k1, u0, u1);
+          if (u0 == u1) A.counters[7] = 1;
+        }
+#endif
         cont = shade(A.S, A.max_depth, P, h, best >= 0, g, L);
       }
     }

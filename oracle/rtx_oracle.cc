@@ -21,7 +21,9 @@
 //   mt      : one std::mt19937 + uniform_real_distribution<double> stream consumed in the
 //             reference's sequential order (random.h:14-32; draw order SURVEY Appendix A.10)
 //   philox  : counter-based Philox-4x32-10 keyed by (seed), counter (draw>>1, sample,
-//             global pixel, 0) — shared bit-for-bit with the HIP kernels (csrc/rtx_rng.h).
+//             global pixel, stream); stream 0 = camera ray, stream n+1 = shading of path
+//             segment n, draw restarting at 0 per stream — shared bit-for-bit with the HIP
+//             kernels (3360-ray-tracer_amd/csrc/rtx_device.h Rng).
 
 #include <algorithm>
 #include <array>
@@ -88,7 +90,7 @@ inline V3 refract(V3 uv, V3 n, double eta) {                          // math_ut
 // RNG
 // ---------------------------------------------------------------------------------------
 struct Philox {
-  // Philox-4x32-10 (Salmon et al., SC'11).  Shared definition with csrc/rtx_rng.h.
+  // Philox-4x32-10 (Salmon et al., SC'11).  Shared definition with csrc/rtx_device.h.
   static void block(uint32_t c[4], uint32_t k0, uint32_t k1) {
     for (int r = 0; r < 10; r++) {
       uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
@@ -110,10 +112,11 @@ struct Rng {
   std::mt19937* mt = nullptr;
   std::uniform_real_distribution<double>* dist = nullptr;
   uint64_t seed = 0;
-  uint32_t pixel = 0, sample = 0, draw = 0;
+  uint32_t pixel = 0, sample = 0, stream = 0, draw = 0;
+  void open(uint32_t s) { stream = s, draw = 0; }  // philox: start stream s at draw 0
   double next() {  // RandomDouble() (random.h:23-26)
     if (mode == 0) return (*dist)(*mt);
-    uint32_t c[4] = {draw >> 1, sample, pixel, 0u};
+    uint32_t c[4] = {draw >> 1, sample, pixel, stream};
     Philox::block(c, (uint32_t)seed, (uint32_t)(seed >> 32) ^ 0x52545831u);
     uint32_t lo = (draw & 1) ? c[2] : c[0];
     uint32_t hi = (draw & 1) ? c[3] : c[1];
@@ -806,6 +809,7 @@ struct PathState {
 };
 
 bool shade(const Scene& S, const Params& P, PathState& ps, const Hit& rec, bool hit, Rng& g, V3& L) {
+  g.open((uint32_t)ps.depth + 1u);  // philox stream of this segment (ignored by mt)
   L = {0, 0, 0};
   if (!hit || ps.depth >= P.max_depth) {
     L = L + ps.thr * sky(ps.d);
@@ -854,7 +858,6 @@ void render_wavefront(const Scene& S, const Camera& cam, const Params& P, double
   struct Q {
     PathState s;
     int pix;
-    uint32_t draw;
   };
   std::vector<Q> q, nq;
   const int min_spp = P.adaptive ? P.min_spp : (1 << 30);
@@ -869,9 +872,9 @@ void render_wavefront(const Scene& S, const Camera& cam, const Params& P, double
         int idx = y * W + x;
         if (px[idx].converged) continue;
         Q e;
-        g.pixel = idx, g.sample = s, g.draw = 0;
+        g.pixel = idx, g.sample = s, g.open(0);
         cam.get_ray(x, y, g, e.s.o, e.s.d);
-        e.pix = idx, e.draw = g.draw;
+        e.pix = idx;
         q.push_back(e);
       }
     st.primaries += (long long)q.size();
@@ -880,10 +883,9 @@ void render_wavefront(const Scene& S, const Camera& cam, const Params& P, double
       for (Q& e : q) {
         Hit rec;
         bool hit = S.hit(e.s.o, e.s.d, (double)0.001f, kInf, rec);
-        g.pixel = e.pix, g.sample = s, g.draw = e.draw;
+        g.pixel = e.pix, g.sample = s;
         V3 L;
         if (shade(S, P, e.s, rec, hit, g, L)) {
-          e.draw = g.draw;
           nq.push_back(e);
         } else {
           finish(px[e.pix], L);
@@ -919,7 +921,7 @@ void render_per_pixel(const Scene& S, const Camera& cam, const Params& P, double
       Rng g;
       g.mode = 1, g.seed = P.seed, g.pixel = idx;
       for (int s = 0; s < P.spp && !ps.converged; s++) {
-        g.sample = s, g.draw = 0;
+        g.sample = s, g.open(0);
         PathState path;
         cam.get_ray(x, y, g, path.o, path.d);
         prim++;
@@ -948,15 +950,16 @@ void render_per_pixel(const Scene& S, const Camera& cam, const Params& P, double
 // Megakernel mode (mega_kernel.h:15-54, DefaultSampler sampler.h:22-34, GetPixel
 // camera.h:148-174): recursive Scatter-API path, interval [0.001, inf) in double, black at
 // depth 0, no RR.  mt mode runs pixels row-major on one thread.
-V3 get_pixel(const Scene& S, V3 o, V3 d, int depth, Rng& g, long long& rays) {
+V3 get_pixel(const Scene& S, V3 o, V3 d, int depth, int max_depth, Rng& g, long long& rays) {
   if (depth <= 0) return {0, 0, 0};
+  g.open((uint32_t)(max_depth - depth) + 1u);  // philox stream of this segment
   Hit rec;
   rays++;
   if (S.hit(o, d, 0.001, kInf, rec)) {
     const Material& m = S.mat[rec.mat];
     V3 att, so, sd;
     V3 em = mat_emitted(S, m, rec.u, rec.v, rec.p);
-    if (mat_scatter(S, m, d, rec, att, so, sd, g)) return em + att * get_pixel(S, so, sd, depth - 1, g, rays);
+    if (mat_scatter(S, m, d, rec, att, so, sd, g)) return em + att * get_pixel(S, so, sd, depth - 1, max_depth, g, rays);
     return em;
   }
   return sky(d);
@@ -978,10 +981,10 @@ void render_megakernel(const Scene& S, const Camera& cam, const Params& P, doubl
       g.mode = P.rng_mode, g.mt = &mt, g.dist = &dist, g.seed = P.seed, g.pixel = y * W + x;
       V3 pixel{0, 0, 0};
       for (int k = 0; k < P.spp; k++) {
-        g.sample = k, g.draw = 0;
+        g.sample = k, g.open(0);
         V3 o, d;
         cam.get_ray(x, y, g, o, d);
-        pixel = pixel + get_pixel(S, o, d, P.max_depth, g, rays);
+        pixel = pixel + get_pixel(S, o, d, P.max_depth, P.max_depth, g, rays);
       }
       pixel = pixel / P.spp;
       size_t oi = (size_t)ty * tw + tx;
@@ -1328,12 +1331,18 @@ int orc_render(void* sp, orc_camera* c, const orc_params* p, double* fb, int* sp
   stats[0] = st.rays, stats[1] = st.primaries;
   return 0;
 }
-// Philox stream check for the GPU RNG: out[i] = RandomDouble for (seed,pixel,sample,draw=i)
-int orc_philox(unsigned long long seed, unsigned pixel, unsigned sample, int n, double* out) {
+// Philox stream check for the GPU RNG: out[i] = RandomDouble for (seed, pixel, sample,
+// stream, draw = i)
+int orc_philox_stream(unsigned long long seed, unsigned pixel, unsigned sample, unsigned stream, int n,
+                      double* out) {
   Rng g;
-  g.mode = 1, g.seed = seed, g.pixel = pixel, g.sample = sample, g.draw = 0;
+  g.mode = 1, g.seed = seed, g.pixel = pixel, g.sample = sample;
+  g.open(stream);
   for (int i = 0; i < n; i++) out[i] = g.next();
   return 0;
+}
+int orc_philox(unsigned long long seed, unsigned pixel, unsigned sample, int n, double* out) {
+  return orc_philox_stream(seed, pixel, sample, 0u, n, out);
 }
 // P3 PPM bytes of a linear framebuffer via write_color (color.h:18-33)
 int orc_write_ppm(const double* fb, int w, int h, const char* path) {

@@ -53,6 +53,7 @@ def lib():
         L.orc_render.argtypes = [C.c_void_p, C.POINTER(OrcCamera), C.POINTER(OrcParams), C.c_void_p, C.c_void_p,
                                  C.c_void_p]
         L.orc_philox.argtypes = [C.c_ulonglong, C.c_uint, C.c_uint, C.c_int, C.c_void_p]
+        L.orc_philox_stream.argtypes = [C.c_ulonglong, C.c_uint, C.c_uint, C.c_uint, C.c_int, C.c_void_p]
         L.orc_write_ppm.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p]
         _lib = L
     return _lib
@@ -171,9 +172,9 @@ def pixelstate(seq):
     return out
 
 
-def philox(seed, pixel, sample, n):
+def philox(seed, pixel, sample, n, stream=0):
     out = np.zeros(n)
-    lib().orc_philox(seed, pixel, sample, n, _ptr(out))
+    lib().orc_philox_stream(seed, pixel, sample, stream, n, _ptr(out))
     return out
 
 
