@@ -140,47 +140,115 @@ int bvh_depth(const rtx_bvh_node* n, int64_t count) {
   }
 }
 
+// Conservative f64 box of one primitive (fast-path leaf splitting).  Spheres: centre +-
+// |r|; rects: the rectangle on its plane; triangles: the vertex box padded by 2^-19 of its
+// largest extent, which covers the points the reference's float-rounded barycentric test
+// accepts just outside the exact triangle (u, v, u + v within 2^-23 of the edges).
+void prim_box(const rtx_prim& p, double lo[3], double hi[3]) {
+  const double* g = p.g;
+  if (p.kind == RTX_PRIM_SPHERE) {
+    const double r = std::fabs(g[3]);
+    for (int a = 0; a < 3; a++) lo[a] = g[a] - r, hi[a] = g[a] + r;
+    return;
+  }
+  if (p.kind == RTX_PRIM_TRIANGLE) {
+    double ext = 0;
+    for (int a = 0; a < 3; a++) {
+      lo[a] = std::min(g[a], std::min(g[3 + a], g[6 + a]));
+      hi[a] = std::max(g[a], std::max(g[3 + a], g[6 + a]));
+      ext = std::max(ext, hi[a] - lo[a]);
+    }
+    const double pad = std::ldexp(ext, -19);
+    for (int a = 0; a < 3; a++) lo[a] -= pad, hi[a] += pad;
+    return;
+  }
+  int ax, a0, a1;  // rect.h: XY (z = k), XZ (y = k), YZ (x = k)
+  if (p.kind == RTX_PRIM_XY_RECT) ax = 2, a0 = 0, a1 = 1;
+  else if (p.kind == RTX_PRIM_XZ_RECT) ax = 1, a0 = 0, a1 = 2;
+  else ax = 0, a0 = 1, a1 = 2;
+  lo[a0] = std::min(g[0], g[1]), hi[a0] = std::max(g[0], g[1]);
+  lo[a1] = std::min(g[2], g[3]), hi[a1] = std::max(g[2], g[3]);
+  lo[ax] = hi[ax] = g[4];
+}
+
 // BVH4 fast layout: the binary tree collapsed top-down.  Each F4Node starts from the binary
-// node's two children and repeatedly opens the internal child with the largest surface area
-// (children stay in left-to-right order) until it holds four slots or only leaves remain.
-// Leaves are the binary leaves, unchanged; every slot keeps its binary node's box, rounded
-// outward.  Returns the exact worst-case traversal stack depth of the collapsed tree
-// (trace_fast4 pushes at most `internal slots - 1` entries per visited node), or -1 when a
-// leaf is too large for the 16-bit slot count.
-[[maybe_unused]] int build_fast4(const rtx_bvh_node* n, std::vector<F4Node>& out) {
+// node's two children and repeatedly opens the slot with the largest surface area until it
+// holds four slots or nothing fits: an internal binary node opens into its two children, a
+// multi-primitive leaf (RTX_LEAF_SPLIT >= 1) into its primitives, each then a one-primitive
+// leaf slot with its own conservative box (prim_box), so the f32 slab test culls primitives
+// before their f64 test.  With RTX_LEAF_SPLIT >= 2 a multi-primitive leaf left in a slot
+// becomes a child F4Node of one-primitive slots.  Every slot keeps a box that contains all
+// hits its primitives can report, rounded outward, so the candidate set is unchanged.
+// Returns the exact worst-case traversal stack depth (trace_fast4 pushes at most
+// `internal slots - 1` entries per visited node), or -1 when a leaf is too large for the
+// 16-bit slot count.
+int build_fast4(const rtx_bvh_node* n, const rtx_prim* prims, std::vector<F4Node>& out) {
   out.clear();
-  auto area = [&](uint32_t i) {
-    const double dx = n[i].hi[0] - n[i].lo[0], dy = n[i].hi[1] - n[i].lo[1], dz = n[i].hi[2] - n[i].lo[2];
+  struct Slot {
+    int kind;  // 0 binary node, 1 primitive, 2 leaf-to-expand (binary leaf as an F4 child)
+    uint32_t id;
+    double lo[3], hi[3];
+  };
+  auto node_slot = [&](uint32_t b) {
+    Slot s{0, b, {}, {}};
+    for (int a = 0; a < 3; a++) s.lo[a] = n[b].lo[a], s.hi[a] = n[b].hi[a];
+    return s;
+  };
+  auto area = [](const Slot& s) {
+    const double dx = s.hi[0] - s.lo[0], dy = s.hi[1] - s.lo[1], dz = s.hi[2] - s.lo[2];
     return dx * dy + dy * dz + dz * dx;
+  };
+  // number of slots a slot opens into (0: cannot open)
+  auto fan = [&](const Slot& s) -> uint32_t {
+    if (s.kind != 0) return 0;
+    if (!n[s.id].is_leaf) return 2;
+    const uint32_t k = n[s.id].right_count;
+    return (RTX_LEAF_SPLIT >= 1 && k >= 2 && k <= 4) ? k : 0;
   };
   int need = 0;
   bool ok = true;
-  // iterative pre-order: (binary node, F4 slot to patch, stack depth on arrival)
   struct Item {
-    uint32_t bin;
+    std::vector<Slot> slots;
     int64_t parent_slot;
     int depth;
   };
-  std::vector<Item> work{{0u, -1, 0}};
+  std::vector<Item> work;
+  work.push_back({{node_slot(n[0].left_first), node_slot(n[0].right_count)}, -1, 0});
   while (!work.empty()) {
-    const Item it = work.back();
+    Item it = std::move(work.back());
     work.pop_back();
     const int32_t me = (int32_t)out.size();
     if (it.parent_slot >= 0) out[it.parent_slot >> 2].child[it.parent_slot & 3] = me;
     out.push_back(F4Node{});
-    std::vector<uint32_t> slots{n[it.bin].left_first, n[it.bin].right_count};
+    std::vector<Slot>& slots = it.slots;
     while (slots.size() < 4) {
       int pick = -1;
       double best = -1.0;
-      for (size_t k = 0; k < slots.size(); k++)
-        if (!n[slots[k]].is_leaf && area(slots[k]) > best) best = area(slots[k]), pick = (int)k;
+      for (size_t k = 0; k < slots.size(); k++) {
+        const uint32_t f = fan(slots[k]);
+        if (f && slots.size() - 1 + f <= 4 && area(slots[k]) > best) best = area(slots[k]), pick = (int)k;
+      }
       if (pick < 0) break;
-      const uint32_t b = slots[pick];
-      slots[pick] = n[b].left_first;
-      slots.insert(slots.begin() + pick + 1, n[b].right_count);
+      const Slot b = slots[pick];
+      std::vector<Slot> rep;
+      if (!n[b.id].is_leaf) {
+        rep = {node_slot(n[b.id].left_first), node_slot(n[b.id].right_count)};
+      } else {
+        for (uint32_t q = 0; q < n[b.id].right_count; q++) {
+          Slot ps{1, n[b.id].left_first + q, {}, {}};
+          prim_box(prims[ps.id], ps.lo, ps.hi);
+          rep.push_back(ps);
+        }
+      }
+      slots.erase(slots.begin() + pick);
+      slots.insert(slots.begin() + pick, rep.begin(), rep.end());
     }
+    for (Slot& sl : slots)  // leaves that stay whole: optionally one more level of prim slots
+      if (RTX_LEAF_SPLIT >= 2 && sl.kind == 0 && n[sl.id].is_leaf && n[sl.id].right_count >= 2 &&
+          n[sl.id].right_count <= 4)
+        sl.kind = 2;
     int internal = 0;
-    for (uint32_t b : slots) internal += n[b].is_leaf ? 0 : 1;
+    for (const Slot& sl : slots) internal += (sl.kind == 2 || (sl.kind == 0 && !n[sl.id].is_leaf)) ? 1 : 0;
     const int child_depth = it.depth + std::max(0, internal - 1);
     need = std::max(need, child_depth);
     F4Node& f = out[me];
@@ -189,18 +257,33 @@ int bvh_depth(const rtx_bvh_node* n, int64_t count) {
         f.child[c] = -1;
         continue;
       }
-      const rtx_bvh_node& cn = n[slots[c]];
-      f.lox[c] = round_down(cn.lo[0]), f.loy[c] = round_down(cn.lo[1]), f.loz[c] = round_down(cn.lo[2]);
-      f.hix[c] = round_up(cn.hi[0]), f.hiy[c] = round_up(cn.hi[1]), f.hiz[c] = round_up(cn.hi[2]);
-      if (cn.is_leaf) {
-        if (cn.right_count > 0xffffu) ok = false;
-        f.child[c] = ~(int32_t)cn.left_first;
-        f.counts[c >> 1] |= (cn.right_count & 0xffffu) << (16 * (c & 1));
-      }
+      const Slot& sl = slots[c];
+      f.lox[c] = round_down(sl.lo[0]), f.loy[c] = round_down(sl.lo[1]), f.loz[c] = round_down(sl.lo[2]);
+      f.hix[c] = round_up(sl.hi[0]), f.hiy[c] = round_up(sl.hi[1]), f.hiz[c] = round_up(sl.hi[2]);
+      uint32_t first = 0, count = 0;
+      if (sl.kind == 1) first = sl.id, count = 1;
+      else if (sl.kind == 0 && n[sl.id].is_leaf) first = n[sl.id].left_first, count = n[sl.id].right_count;
+      else continue;  // internal: patched when the child is emitted
+      if (count > 0xffffu) ok = false;
+      f.child[c] = ~(int32_t)first;
+      f.counts[c >> 1] |= (count & 0xffffu) << (16 * (c & 1));
     }
     // push in reverse so children are laid out in slot order (pre-order)
-    for (int c = (int)slots.size() - 1; c >= 0; c--)
-      if (!n[slots[c]].is_leaf) work.push_back({slots[c], (int64_t)me * 4 + c, child_depth});
+    for (int c = (int)slots.size() - 1; c >= 0; c--) {
+      const Slot& sl = slots[c];
+      if (sl.kind == 2) {
+        std::vector<Slot> ps;
+        for (uint32_t q = 0; q < n[sl.id].right_count; q++) {
+          Slot p1{1, n[sl.id].left_first + q, {}, {}};
+          prim_box(prims[p1.id], p1.lo, p1.hi);
+          ps.push_back(p1);
+        }
+        work.push_back({std::move(ps), (int64_t)me * 4 + c, child_depth});
+      } else if (sl.kind == 0 && !n[sl.id].is_leaf) {
+        work.push_back({{node_slot(n[sl.id].left_first), node_slot(n[sl.id].right_count)}, (int64_t)me * 4 + c,
+                        child_depth});
+      }
+    }
   }
   return ok ? need : -1;
 }
@@ -342,6 +425,7 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   if (d->n_prims < 0 || d->n_nodes < 0 || d->n_materials < 0 || d->n_textures < 0 || d->n_images < 0)
     return fail(RTX_ERR_INVALID, "negative counts");
   if (d->n_prims > 0 && !d->prims) return fail(RTX_ERR_INVALID, "prims is NULL");
+  if (d->n_prims > 0x7FFFFFFFll) return fail(RTX_ERR_INVALID, "more than 2^31-1 primitives");
   // validate indices so kernels never read out of bounds
   for (int64_t i = 0; i < d->n_prims; i++) {
     const rtx_prim& p = d->prims[i];
@@ -408,7 +492,7 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
     if (sc->stack_parity < 0) return fail(RTX_ERR_INVALID, "BVH deeper than 62 levels");
     if (!d->nodes[0].is_leaf) {
 #if RTX_BVH4
-      const int need = build_fast4(d->nodes, f4);
+      const int need = build_fast4(d->nodes, d->prims, f4);
       sc->stack_fast = need < 0 ? -1 : (need <= 32 ? 32 : (need <= 64 ? 64 : -1));
       if (sc->stack_fast > 0 && (rc = upload(sc->fnodes, f4.data(), f4.size(), s))) return rc;
 #else
@@ -687,7 +771,7 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
     HIPC(hipEventSynchronize(sc->ev[1]));
     float ms = 0;
     HIPC(hipEventElapsedTime(&ms, sc->ev[0], sc->ev[1]));
-    unsigned long long h[4];
+    unsigned long long h[6];
     HIPC(hipMemcpy(h, cnt, sizeof h, hipMemcpyDeviceToHost));
     stats->rays_total = h[0];
     stats->rays_primary = h[1];
@@ -697,6 +781,8 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
     stats->hot_launches = hot_launches;
     stats->node_visits = h[2];
     stats->prim_tests = h[3];
+    stats->wave_node_iters = h[4];
+    stats->wave_prim_iters = h[5];
     stats->node_bytes = (L.fast && RTX_BVH4) ? sizeof(F4Node) : (L.fast ? sizeof(FNode) : sizeof(rtx_bvh_node));
   }
   return RTX_OK;

@@ -12,10 +12,6 @@
 
 #include "rtx.h"
 
-// timing experiments only (tests fail with these): upper bounds of the RNG / trig cost
-#ifndef RTX_X_PHILOX_ROUNDS
-#define RTX_X_PHILOX_ROUNDS 10
-#endif
 #ifndef RTX_PHILOX_MAD
 #define RTX_PHILOX_MAD 1  // A/B r01: +2.3% C2, neutral bunny
 #endif
@@ -79,7 +75,7 @@ __device__ __forceinline__ void philox_block(uint32_t blk, uint32_t sample, uint
   uint32_t c0 = blk, c1 = sample, c2 = pixel, c3 = stream;
   uint32_t a = k0, b = k1;
 #pragma unroll
-  for (int r = 0; r < RTX_X_PHILOX_ROUNDS; r++) {
+  for (int r = 0; r < 10; r++) {
 #if RTX_PHILOX_MAD
     // one v_mad_u64_u32 per product instead of v_mul_lo_u32 + v_mul_hi_u32
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
@@ -150,13 +146,8 @@ __device__ __forceinline__ V3 random_cosine_direction(Rng& g, V3 normal) {  // m
   double r2 = g.next();
   double phi = 2.0 * kPi * r1;
   double r = sqrt(r2);
-#if RTX_X_F32TRIG
-  double x = r * (double)cosf((float)phi);
-  double y = r * (double)sinf((float)phi);
-#else
   double x = r * cos(phi);
   double y = r * sin(phi);
-#endif
   double z = sqrt(1.0 - r2);
   V3 w = normalize(normal);
   V3 a = (fabs(w.x) > 0.9) ? v3(0, 1, 0) : v3(1, 0, 0);
@@ -418,8 +409,14 @@ __device__ __forceinline__ bool box_hit(const double* lo, const double* hi, V3 o
 }
 
 struct Counters {
-  uint32_t nodes, prims;
+  uint32_t nodes, prims;  // lane-level node visits / primitive tests
+  uint32_t wnodes, wprims;  // wave-level loop iterations (counted by the first active lane)
 };
+// first active lane of the (possibly divergent) wave
+__device__ __forceinline__ bool first_active_lane() {
+  const unsigned long long m = __ballot(1);
+  return (int)__lane_id() == __ffsll((long long)m) - 1;
+}
 
 // ---------------------------------------------------------------------------------------
 // Parity traversal: Scene{Bvh}::Hit exactly as bvh.h:71-119 (stack, push right then left,
@@ -656,7 +653,10 @@ __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, doub
   int32_t node = 0;
   while (true) {
     const F4Node* __restrict__ nd = S.f4nodes + node;
-    if (COUNT) cnt.nodes++;
+    if (COUNT) {
+      cnt.nodes++;
+      if (first_active_lane()) cnt.wnodes++;
+    }
     float tt[4];
     int32_t cc[4];
     const uint32_t counts01 = nd->counts[0], counts23 = nd->counts[1];
@@ -686,7 +686,10 @@ __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, doub
           cur = (uint32_t)(~ch);
           left = ((c < 2 ? counts01 : counts23) >> (16 * (c & 1))) & 0xffffu;
         }
-        if (COUNT) cnt.prims++;
+        if (COUNT) {
+          cnt.prims++;
+          if (first_active_lane()) cnt.wprims++;
+        }
         if (prim_t(S.prims + cur, o, d, tmin, closest, t)) closest = t, best = (int64_t)cur, shrink = true;
         cur++, left--;
       }

@@ -24,6 +24,9 @@ constexpr int kBlock = 256;
 #ifndef RTX_TRACE_WAVES
 #define RTX_TRACE_WAVES 4  // min waves per SIMD for the trace kernels (<= 128 VGPRs; measured best)
 #endif
+#ifndef RTX_LEAF_SPLIT
+#define RTX_LEAF_SPLIT 2  // BVH4 (A/B r01: 2 = +15% C2, +24% bunny): 0 keep the reference's leaves, 1 open them into one-primitive slots, 2 also as child nodes
+#endif
 #ifndef RTX_BVH4
 #define RTX_BVH4 1  // fast precision traverses the 4-wide collapse of the SAH tree (else BVH2)
 #endif
@@ -106,6 +109,8 @@ __device__ __forceinline__ void flush_counters(const RenderArgs& A, const Counte
   if (count) {
     atomicAdd(&A.counters[2], (unsigned long long)c.nodes);
     atomicAdd(&A.counters[3], (unsigned long long)c.prims);
+    atomicAdd(&A.counters[4], (unsigned long long)c.wnodes);
+    atomicAdd(&A.counters[5], (unsigned long long)c.wprims);
   }
   if (segs) atomicAdd(&A.counters[0], (unsigned long long)segs);
   if (prims) atomicAdd(&A.counters[1], (unsigned long long)prims);
@@ -124,7 +129,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_intersect(DScene S,
   if (i >= n) return;
   const rtx_ray r = rays[i];
   V3 o{r.origin[0], r.origin[1], r.origin[2]}, d{r.direction[0], r.direction[1], r.direction[2]};
-  Counters c{0, 0};
+  Counters c{0, 0, 0, 0};
   const int64_t best = trace<STACK, FAST, false>(S, o, d, tmin, tmax, stk, c);
   rtx_hit out;
   out.pad_ = 0;
@@ -174,7 +179,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_generate(RenderArgs A, PathQueue 
       q.meta[dst] = 0u;  // depth 0
     }
   }
-  flush_counters(A, Counters{0, 0}, 0, made, false);
+  flush_counters(A, Counters{0, 0, 0, 0}, 0, made, false);
 }
 
 // Closest hit for every queued path (one ray per lane, grid-stride).
@@ -184,7 +189,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_wf_extend(RenderArg
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* stk = lds + threadIdx.x;
   const int64_t n = *count;
-  Counters c{0, 0};
+  Counters c{0, 0, 0, 0};
   uint32_t segs = 0;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
     const V3 o = v3(q.ox[i], q.oy[i], q.oz[i]);
@@ -252,7 +257,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
   const uint64_t nslots = (uint64_t)A.npix * (uint64_t)A.K;
   // GetPixel uses Interval(0.001, inf) (camera.h:158); IntersectBatch uses 0.001f (cpu_ray_integrator.h:21)
   const double tmin = SCATTER ? 0.001 : (double)0.001f;
-  Counters c{0, 0};
+  Counters c{0, 0, 0, 0};
   uint32_t segs = 0, prims = 0;
   uint64_t chunk_base = 0, chunk_left = 0;  // wave-uniform
   bool exhausted = false;                   // wave-uniform
@@ -321,14 +326,6 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
     } else {
       const int64_t best = trace<STACK, FAST, COUNT>(A.S, P.o, P.d, tmin, kInf, stk, c);
       segs++;
-#if RTX_X_DUP_TRACE  // timing experiment: marginal cost of one more traversal
-      {
-        V3 od = P.d;
-        asm volatile("" : "+v"(od.x));
-        const int64_t b2 = trace<STACK, FAST, COUNT>(A.S, P.o, od, tmin, kInf, stk, c);
-        if (b2 == -7) A.counters[7] = 1;
-      }
-#endif
       Hit h;
       if (best >= 0) finish_hit<false>(A.S, best, P.o, P.d, tmin, h);
       // stream of this segment: depth + 1 (GetPixel: depth counts down from max_depth)
@@ -354,25 +351,6 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
           }
         }
       } else {
-#if RTX_X_DUP_SHADE  // timing experiment: marginal cost of one more shading step
-        {
-          Path P2 = P;
-          asm volatile("" : "+v"(P2.d.x));
-          Rng g2 = g;
-          V3 L2;
-          const bool c2 = shade(A.S, A.max_depth, P2, h, best >= 0, g2, L2);
-          if (c2 && L2.x == -7.0 && P2.d.y == -7.0) A.counters[7] = 1;
-        }
-#endif
-#if RTX_X_DUP_RNG  // timing experiment: marginal cost of one more Philox block
-        {
-          uint32_t s2 = smp;
-          asm volatile("" : "+v"(s2));
-          double u0, u1;
-          philox_block(1u, s2, pix, (uint32_t)P.depth + 1u, g.k0, g.k1, u0, u1);
-          if (u0 == u1) A.counters[7] = 1;
-        }
-#endif
         cont = shade(A.S, A.max_depth, P, h, best >= 0, g, L);
       }
     }

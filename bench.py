@@ -128,6 +128,9 @@ def main():
     p.flags = 0
     segs = max(1, cst["rays_total"])
     nodes_per_seg = cst["node_visits"] / segs
+    # SIMD efficiency of the traversal loops (fast BVH4 only): lane work / (64 x wave iterations)
+    simd_nodes = cst["node_visits"] / (64.0 * cst["wave_node_iters"]) if cst["wave_node_iters"] else None
+    simd_prims = cst["prim_tests"] / (64.0 * cst["wave_prim_iters"]) if cst["wave_prim_iters"] else None
     prims_per_seg = cst["prim_tests"] / segs
     node_bytes = cst["node_bytes"]  # fast: F4Node 128 B (4 f32 child boxes); parity: rtx_bvh_node 64 B
     prim_bytes = 80  # rtx_prim (f64 geometry + kind/material)
@@ -167,7 +170,8 @@ def main():
                          "kernel": "k_persistent" if args.mode == "persistent" else "k_wf_bounce",
                          "avg_launch_ms": avg_launch_s * 1e3, "segments_per_launch": segs_per_launch,
                          "bytes_per_segment": bytes_per_seg, "nodes_per_segment": nodes_per_seg,
-                         "prims_per_segment": prims_per_seg},
+                         "prims_per_segment": prims_per_seg, "simd_efficiency_nodes": simd_nodes,
+                         "simd_efficiency_prims": simd_prims},
             "rays_per_step": rays_all / args.steps,
         }
         if not args.no_cpu_baseline and world == 1:
