@@ -771,7 +771,7 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
     HIPC(hipEventSynchronize(sc->ev[1]));
     float ms = 0;
     HIPC(hipEventElapsedTime(&ms, sc->ev[0], sc->ev[1]));
-    unsigned long long h[6];
+    unsigned long long h[8];
     HIPC(hipMemcpy(h, cnt, sizeof h, hipMemcpyDeviceToHost));
     stats->rays_total = h[0];
     stats->rays_primary = h[1];
@@ -783,6 +783,8 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
     stats->prim_tests = h[3];
     stats->wave_node_iters = h[4];
     stats->wave_prim_iters = h[5];
+    stats->tri_tests = h[6];
+    stats->sphere_tests = h[7];
     stats->node_bytes = (L.fast && RTX_BVH4) ? sizeof(F4Node) : (L.fast ? sizeof(FNode) : sizeof(rtx_bvh_node));
   }
   return RTX_OK;

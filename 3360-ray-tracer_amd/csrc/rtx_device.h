@@ -411,7 +411,14 @@ __device__ __forceinline__ bool box_hit(const double* lo, const double* hi, V3 o
 struct Counters {
   uint32_t nodes, prims;  // lane-level node visits / primitive tests
   uint32_t wnodes, wprims;  // wave-level loop iterations (counted by the first active lane)
+  uint32_t tris, sphs;      // primitive tests by kind (rects = prims - tris - sphs)
 };
+__device__ __forceinline__ void count_prim(Counters& c, const rtx_prim* P) {
+  c.prims++;
+  const int k = P->kind;
+  c.tris += k == RTX_PRIM_TRIANGLE ? 1u : 0u;
+  c.sphs += k == RTX_PRIM_SPHERE ? 1u : 0u;
+}
 // first active lane of the (possibly divergent) wave
 __device__ __forceinline__ bool first_active_lane() {
   const unsigned long long m = __ballot(1);
@@ -431,7 +438,7 @@ __device__ __forceinline__ int64_t trace_parity(const DScene& S, V3 o, V3 d, dou
   double closest = tmax, t;
   if (!S.use_bvh) {  // scene::Scene::Hit linear list (scene.h:47-61)
     for (int64_t i = 0; i < S.n_prims; i++) {
-      if (COUNT) cnt.prims++;
+      if (COUNT) count_prim(cnt, S.prims + i);
       if (prim_t(S.prims + i, o, d, tmin, closest, t)) closest = t, best = i;
     }
     return best;
@@ -449,7 +456,7 @@ __device__ __forceinline__ int64_t trace_parity(const DScene& S, V3 o, V3 d, dou
     if (!box_hit(lo, hi, o, o, d, tmin, closest)) continue;
     if (leaf) {
       for (uint32_t i = 0; i < b; i++) {
-        if (COUNT) cnt.prims++;
+        if (COUNT) count_prim(cnt, S.prims + a + i);
         if (prim_t(S.prims + a + i, o, d, tmin, closest, t)) closest = t, best = (int64_t)a + i;
       }
     } else {
@@ -511,7 +518,7 @@ __device__ __forceinline__ int64_t trace_fast(const DScene& S, V3 o, V3 d, doubl
   if (!S.use_bvh || S.froot_leaf) {
     const int64_t n = S.use_bvh ? S.froot_count : S.n_prims;
     for (int64_t i = 0; i < n; i++) {
-      if (COUNT) cnt.prims++;
+      if (COUNT) count_prim(cnt, S.prims + i);
       if (prim_t(S.prims + i, o, d, tmin, closest, t)) closest = t, best = i;
     }
     return best;
@@ -536,7 +543,7 @@ __device__ __forceinline__ int64_t trace_fast(const DScene& S, V3 o, V3 d, doubl
     if (h0 && c0 < 0) {
       uint32_t first = (uint32_t)(~c0);
       for (uint32_t i = 0; i < n0; i++) {
-        if (COUNT) cnt.prims++;
+        if (COUNT) count_prim(cnt, S.prims + first + i);
         if (prim_t(S.prims + first + i, o, d, tmin, closest, t)) closest = t, best = (int64_t)first + i, shrink = true;
       }
       h0 = false;
@@ -544,7 +551,7 @@ __device__ __forceinline__ int64_t trace_fast(const DScene& S, V3 o, V3 d, doubl
     if (h1 && c1 < 0) {
       uint32_t first = (uint32_t)(~c1);
       for (uint32_t i = 0; i < n1; i++) {
-        if (COUNT) cnt.prims++;
+        if (COUNT) count_prim(cnt, S.prims + first + i);
         if (prim_t(S.prims + first + i, o, d, tmin, closest, t)) closest = t, best = (int64_t)first + i, shrink = true;
       }
       h1 = false;
@@ -642,7 +649,7 @@ __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, doub
   if (!S.use_bvh || S.froot_leaf) {
     const int64_t n = S.use_bvh ? S.froot_count : S.n_prims;
     for (int64_t i = 0; i < n; i++) {
-      if (COUNT) cnt.prims++;
+      if (COUNT) count_prim(cnt, S.prims + i);
       if (prim_t(S.prims + i, o, d, tmin, closest, t)) closest = t, best = i;
     }
     return best;
@@ -687,7 +694,7 @@ __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, doub
           left = ((c < 2 ? counts01 : counts23) >> (16 * (c & 1))) & 0xffffu;
         }
         if (COUNT) {
-          cnt.prims++;
+          count_prim(cnt, S.prims + cur);
           if (first_active_lane()) cnt.wprims++;
         }
         if (prim_t(S.prims + cur, o, d, tmin, closest, t)) closest = t, best = (int64_t)cur, shrink = true;

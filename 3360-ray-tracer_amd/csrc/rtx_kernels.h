@@ -111,6 +111,8 @@ __device__ __forceinline__ void flush_counters(const RenderArgs& A, const Counte
     atomicAdd(&A.counters[3], (unsigned long long)c.prims);
     atomicAdd(&A.counters[4], (unsigned long long)c.wnodes);
     atomicAdd(&A.counters[5], (unsigned long long)c.wprims);
+    atomicAdd(&A.counters[6], (unsigned long long)c.tris);
+    atomicAdd(&A.counters[7], (unsigned long long)c.sphs);
   }
   if (segs) atomicAdd(&A.counters[0], (unsigned long long)segs);
   if (prims) atomicAdd(&A.counters[1], (unsigned long long)prims);
@@ -129,7 +131,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_intersect(DScene S,
   if (i >= n) return;
   const rtx_ray r = rays[i];
   V3 o{r.origin[0], r.origin[1], r.origin[2]}, d{r.direction[0], r.direction[1], r.direction[2]};
-  Counters c{0, 0, 0, 0};
+  Counters c{0, 0, 0, 0, 0, 0};
   const int64_t best = trace<STACK, FAST, false>(S, o, d, tmin, tmax, stk, c);
   rtx_hit out;
   out.pad_ = 0;
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_generate(RenderArgs A, PathQueue 
       q.meta[dst] = 0u;  // depth 0
     }
   }
-  flush_counters(A, Counters{0, 0, 0, 0}, 0, made, false);
+  flush_counters(A, Counters{0, 0, 0, 0, 0, 0}, 0, made, false);
 }
 
 // Closest hit for every queued path (one ray per lane, grid-stride).
@@ -189,7 +191,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_wf_extend(RenderArg
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* stk = lds + threadIdx.x;
   const int64_t n = *count;
-  Counters c{0, 0, 0, 0};
+  Counters c{0, 0, 0, 0, 0, 0};
   uint32_t segs = 0;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
     const V3 o = v3(q.ox[i], q.oy[i], q.oz[i]);
@@ -257,7 +259,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
   const uint64_t nslots = (uint64_t)A.npix * (uint64_t)A.K;
   // GetPixel uses Interval(0.001, inf) (camera.h:158); IntersectBatch uses 0.001f (cpu_ray_integrator.h:21)
   const double tmin = SCATTER ? 0.001 : (double)0.001f;
-  Counters c{0, 0, 0, 0};
+  Counters c{0, 0, 0, 0, 0, 0};
   uint32_t segs = 0, prims = 0;
   uint64_t chunk_base = 0, chunk_left = 0;  // wave-uniform
   bool exhausted = false;                   // wave-uniform

@@ -90,7 +90,8 @@ class Stats(C.Structure):
     _fields_ = [("rays_primary", C.c_uint64), ("rays_total", C.c_uint64), ("paths", C.c_uint64),
                 ("kernel_ms", C.c_double), ("hot_kernel_ms", C.c_double), ("hot_launches", C.c_uint64),
                 ("node_visits", C.c_uint64), ("prim_tests", C.c_uint64),
-                ("node_bytes", C.c_uint64), ("wave_node_iters", C.c_uint64), ("wave_prim_iters", C.c_uint64)]
+                ("node_bytes", C.c_uint64), ("wave_node_iters", C.c_uint64), ("wave_prim_iters", C.c_uint64),
+                ("tri_tests", C.c_uint64), ("sphere_tests", C.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

@@ -132,17 +132,32 @@ def main():
     simd_nodes = cst["node_visits"] / (64.0 * cst["wave_node_iters"]) if cst["wave_node_iters"] else None
     simd_prims = cst["prim_tests"] / (64.0 * cst["wave_prim_iters"]) if cst["wave_prim_iters"] else None
     prims_per_seg = cst["prim_tests"] / segs
-    node_bytes = cst["node_bytes"]  # fast: F4Node 128 B (4 f32 child boxes); parity: rtx_bvh_node 64 B
-    prim_bytes = 80  # rtx_prim (f64 geometry + kind/material)
-    state_bytes = 48 if args.mode == "persistent" else 48 + 88 + 88  # material 48 (+ SoA path state in/out)
-    bytes_per_seg = node_bytes * nodes_per_seg + prim_bytes * prims_per_seg + state_bytes
+    # B_seg = 32*n_box + 48*n_tri + 16*n_sph + 32*n_rect + 96 (path state in + out).
+    # One box = one 32-B node of the compact model; a visit of the 128-B F4Node tests four boxes,
+    # of the 64-B BVH2 FNode two, of the reference-layout f64 node (parity) one.
+    boxes_per_visit = 1 if args.precision == "parity" else cst["node_bytes"] // 32
+    tris_per_seg = cst["tri_tests"] / segs
+    sphs_per_seg = cst["sphere_tests"] / segs
+    rects_per_seg = max(0.0, prims_per_seg - tris_per_seg - sphs_per_seg)
+    bytes_per_seg = (32 * boxes_per_visit * nodes_per_seg + 48 * tris_per_seg + 16 * sphs_per_seg
+                     + 32 * rects_per_seg + 96)
     segs_per_launch = rays / max(1, hot_launches)
     avg_launch_s = hot_ms / 1e3 / max(1, hot_launches)
     achieved_gbs = bytes_per_seg * segs_per_launch / avg_launch_s / 1e9
-    traffic = None
+    traffic = valu = None
     tf = os.path.join(ROOT, "profiles", f"traffic_{args.workload}_{args.mode}_{args.precision}.json")
     if os.path.exists(tf):
-        traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
+        prof = json.load(open(tf))
+        traffic = prof.get("hbm_bytes_per_launch")
+        if prof.get("valu_insts_per_launch"):
+            # VALU issue (the kernel's actual limiter; the scene is L2/MALL-resident): wave64
+            # VALU instructions per launch from the committed PMC profile of this build, over
+            # the live launch time; peak = 1 wave-instruction / 2 cycles / SIMD (SIMD-32,
+            # MI355X_MICROARCH.md) x 1024 SIMDs x 2.4 GHz
+            v_rate = prof["valu_insts_per_launch"] / avg_launch_s
+            v_peak = 1024 * 2.4e9 / 2
+            valu = {"achieved": v_rate, "peak": v_peak, "unit": "wave-instr/s", "frac": v_rate / v_peak,
+                    "source": prof.get("source")}
 
     out = None
     if rank == 0:
@@ -170,8 +185,12 @@ def main():
                          "kernel": "k_persistent" if args.mode == "persistent" else "k_wf_bounce",
                          "avg_launch_ms": avg_launch_s * 1e3, "segments_per_launch": segs_per_launch,
                          "bytes_per_segment": bytes_per_seg, "nodes_per_segment": nodes_per_seg,
-                         "prims_per_segment": prims_per_seg, "simd_efficiency_nodes": simd_nodes,
-                         "simd_efficiency_prims": simd_prims},
+                         "prims_per_segment": prims_per_seg, "tris_per_segment": tris_per_seg,
+                         "spheres_per_segment": sphs_per_seg, "boxes_per_visit": boxes_per_visit,
+                         "simd_efficiency_nodes": simd_nodes, "simd_efficiency_prims": simd_prims,
+                         "valu": valu,
+                         "note": "algorithmic bytes per SURVEY 8(d); the scene is L2/MALL-resident, so "
+                                 "HBM traffic (PMC) << algorithmic bytes and frac may exceed 1"},
             "rays_per_step": rays_all / args.steps,
         }
         if not args.no_cpu_baseline and world == 1:

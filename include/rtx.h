@@ -206,6 +206,8 @@ typedef struct {
   uint64_t node_bytes;     /* bytes of one BVH node visit in the traversal used (64 BVH2, 128 BVH4) */
   uint64_t wave_node_iters; /* with RTX_FLAG_COUNT, fast BVH4: node-loop iterations per wave (SIMD efficiency */
   uint64_t wave_prim_iters; /*   = node_visits / (64 * wave_node_iters)); primitive-loop iterations per wave */
+  uint64_t tri_tests;       /* with RTX_FLAG_COUNT: triangle / sphere tests among prim_tests (rest: rects) */
+  uint64_t sphere_tests;
 } rtx_stats;
 
 /* ---- entry points ------------------------------------------------------------------ */

@@ -50,7 +50,11 @@ def main():
             n_f = len(launches[(k, "FETCH_SIZE")])
             n_w = len(launches[(k, "WRITE_SIZE")])
             per = v["FETCH_SIZE"] * 2 * 1024 / n_f + v["WRITE_SIZE"] * 1024 / n_w
-            t = {"kernel": k, "hbm_bytes_per_launch": per, "fetch_kib_total": v["FETCH_SIZE"],
+            valu = None
+            if "SQ_INSTS_VALU" in v:
+                valu = v["SQ_INSTS_VALU"] / max(1, len(launches[(k, "SQ_INSTS_VALU")]))
+            t = {"kernel": k, "hbm_bytes_per_launch": per, "valu_insts_per_launch": valu,
+                 "fetch_kib_total": v["FETCH_SIZE"],
                  "write_kib_total": v["WRITE_SIZE"], "launches_fetch_pass": n_f, "launches_write_pass": n_w,
                  "source": f"profiles/{rnd}/pmc_{tag}.json", "correction": "FETCH_SIZE x2 (gfx950)"}
             json.dump(t, open(os.path.join(ROOT, "profiles", f"traffic_{workload}_{mode}_{prec}.json"), "w"),
