@@ -13,6 +13,7 @@
 
 #include "rtx.h"
 #include "rtx_kernels.h"
+#include "rtx_p3.h"
 
 using namespace rtxd;
 
@@ -81,13 +82,15 @@ struct rtx_scene {
   int64_t n_nodes = 0;
   // render workspace (grow-only)
   DevBuf px_sum, px_mean, px_m2, px_samples, px_conv, lbuf, queue[2], counters, out_rgb, out_spp, rays, hits;
+  DevBuf p3_scratch, p3_body;  // device P3 encoding (rtx_p3.h)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> evpool;
   ~rtx_scene() {
     for (auto e : evpool) (void)hipEventDestroy(e);
     (void)hipSetDevice(device);
     for (DevBuf* b : {&nodes, &prims, &mats, &texs, &images, &fnodes, &px_sum, &px_mean, &px_m2, &px_samples,
-                      &px_conv, &lbuf, &queue[0], &queue[1], &counters, &out_rgb, &out_spp, &rays, &hits})
+                      &px_conv, &lbuf, &queue[0], &queue[1], &counters, &out_rgb, &out_spp, &rays, &hits, &p3_scratch,
+                      &p3_body})
       b->release();
     for (auto& t : texels) t.release();
     for (auto& e : ev)
@@ -806,6 +809,69 @@ int rtx_render(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* pr
   HIPC(hipMemcpyAsync(rgb, sc->out_rgb.p, npix * 3 * sizeof(double), hipMemcpyDeviceToHost, sc->stream));
   if (spp) HIPC(hipMemcpyAsync(spp, sc->out_spp.p, npix * sizeof(int32_t), hipMemcpyDeviceToHost, sc->stream));
   HIPC(hipStreamSynchronize(sc->stream));
+  return RTX_OK;
+}
+
+// ---- P3 output on the device (wavefront.cc:238-241, core/color.h:18-33) ----
+static std::string p3_header(int64_t w, int64_t h) {
+  return "P3\n" + std::to_string(w) + " " + std::to_string(h) + "\n255\n";
+}
+
+size_t rtx_p3_max_bytes(int32_t w, int32_t h) {
+  if (w <= 0 || h <= 0) return 0;
+  return p3_header(w, h).size() + (size_t)w * (size_t)h * rtxp3::kMaxLine;
+}
+
+// body of d_rgb into sc->p3_body; *len = body bytes
+static int p3_encode(rtx_scene* sc, const double* d_rgb, int64_t npix, size_t* len, hipStream_t s) {
+  if ((uint64_t)npix * rtxp3::kMaxLine > 0xFFFFFFFFull) return fail(RTX_ERR_INVALID, "P3 output above 4 GiB");
+  int rc;
+  if ((rc = sc->p3_scratch.reserve(rtxp3::scratch_bytes(std::max<int64_t>(1, npix))))) return rc;
+  if ((rc = sc->p3_body.reserve(std::max<int64_t>(1, npix) * rtxp3::kMaxLine))) return rc;
+  HIPC(rtxp3::encode_body(d_rgb, npix, sc->p3_scratch.p, (char*)sc->p3_body.p, len, s));
+  return RTX_OK;
+}
+
+int rtx_encode_p3_device(rtx_scene* sc, const double* d_rgb, int32_t w, int32_t h, char* d_out, size_t cap,
+                         size_t* out_len, void* stream) {
+  if (!sc || !d_rgb || !d_out || !out_len || w <= 0 || h <= 0) return fail(RTX_ERR_INVALID, "bad argument");
+  if (cap < rtx_p3_max_bytes(w, h)) return fail(RTX_ERR_INVALID, "output buffer below rtx_p3_max_bytes");
+  HIPC(hipSetDevice(sc->device));
+  hipStream_t s = stream ? (hipStream_t)stream : sc->stream;
+  const std::string hd = p3_header(w, h);
+  size_t body = 0;
+  int rc;
+  if ((rc = p3_encode(sc, d_rgb, (int64_t)w * h, &body, s))) return rc;
+  HIPC(hipMemcpyAsync(d_out, hd.data(), hd.size(), hipMemcpyHostToDevice, s));
+  HIPC(hipMemcpyAsync(d_out + hd.size(), sc->p3_body.p, body, hipMemcpyDeviceToDevice, s));
+  HIPC(hipStreamSynchronize(s));
+  *out_len = hd.size() + body;
+  return RTX_OK;
+}
+
+int rtx_render_p3(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm, char* out, size_t cap,
+                  size_t* out_len, double* rgb, int32_t* spp, rtx_stats* stats) {
+  if (!sc || !cam || !prm || !out || !out_len) return fail(RTX_ERR_INVALID, "NULL argument");
+  PixelMap map;
+  std::string err;
+  const int64_t npix = subset_pixels(cam, prm, map, err);
+  if (npix < 0) return fail(RTX_ERR_INVALID, err);
+  const std::string hd = p3_header(map.w, map.h);
+  if (cap < hd.size() + (size_t)npix * rtxp3::kMaxLine) return fail(RTX_ERR_INVALID, "output buffer below rtx_p3_max_bytes");
+  HIPC(hipSetDevice(sc->device));
+  int rc;
+  if ((rc = sc->out_rgb.reserve(std::max<int64_t>(1, npix) * 3 * sizeof(double)))) return rc;
+  if ((rc = sc->out_spp.reserve(std::max<int64_t>(1, npix) * sizeof(int32_t)))) return rc;
+  if ((rc = rtx_render_device(sc, cam, prm, sc->out_rgb.as<double>(), sc->out_spp.as<int32_t>(), stats, sc->stream)))
+    return rc;
+  size_t body = 0;
+  if ((rc = p3_encode(sc, sc->out_rgb.as<double>(), npix, &body, sc->stream))) return rc;
+  std::memcpy(out, hd.data(), hd.size());
+  HIPC(hipMemcpyAsync(out + hd.size(), sc->p3_body.p, body, hipMemcpyDeviceToHost, sc->stream));
+  if (rgb) HIPC(hipMemcpyAsync(rgb, sc->out_rgb.p, npix * 3 * sizeof(double), hipMemcpyDeviceToHost, sc->stream));
+  if (spp) HIPC(hipMemcpyAsync(spp, sc->out_spp.p, npix * sizeof(int32_t), hipMemcpyDeviceToHost, sc->stream));
+  HIPC(hipStreamSynchronize(sc->stream));
+  *out_len = hd.size() + body;
   return RTX_OK;
 }
 

@@ -85,11 +85,12 @@ void WavefrontRenderer::Render(std::ostream& out) {
   const int64_t n = (int64_t)dc.image_width * dc.image_height;
   rgb_.assign(3 * n, 0.0);
   spp_.assign(n, 0);
-  if (rtx_render(gpu->device_scene(), &dc, &p, rgb_.data(), spp_.data(), &stats_) != RTX_OK)
-    throw std::runtime_error(std::string("rtx_render: ") + rtx_last_error());
-  // wavefront.cc:238-241
-  out << "P3\n" << dc.image_width << ' ' << dc.image_height << "\n255\n";
-  for (int64_t k = 0; k < n; k++) core::write_color(out, core::Color(rgb_[3 * k], rgb_[3 * k + 1], rgb_[3 * k + 2]));
+  // wavefront.cc:238-241: the P3 text is formatted on the device (rtx_render_p3)
+  std::string bytes(rtx_p3_max_bytes(dc.image_width, dc.image_height), '\0');
+  size_t len = 0;
+  if (rtx_render_p3(gpu->device_scene(), &dc, &p, bytes.data(), bytes.size(), &len, rgb_.data(), spp_.data(), &stats_) != RTX_OK)
+    throw std::runtime_error(std::string("rtx_render_p3: ") + rtx_last_error());
+  out.write(bytes.data(), (std::streamsize)len);
 }
 
 MegaKernel::MegaKernel(scene::Scene& scene, scene::Camera& camera, integrator::Sampler& sampler, int device)
@@ -105,13 +106,13 @@ void MegaKernel::Render(std::ostream& out) {
   p.adaptive = 0;
   p.mode = RTX_MODE_MEGAKERNEL;
   p.seed = seed_;
-  const int64_t n = (int64_t)dc.image_width * dc.image_height;
-  rgb_.assign(3 * n, 0.0);
   rtx_stats st{};
-  if (rtx_render(gpu.device_scene(), &dc, &p, rgb_.data(), nullptr, &st) != RTX_OK)
-    throw std::runtime_error(std::string("rtx_render: ") + rtx_last_error());
-  out << "P3\n" << dc.image_width << ' ' << dc.image_height << "\n255\n";
-  for (int64_t k = 0; k < n; k++) core::write_color(out, core::Color(rgb_[3 * k], rgb_[3 * k + 1], rgb_[3 * k + 2]));
+  rgb_.assign(3 * (size_t)dc.image_width * dc.image_height, 0.0);
+  std::string bytes(rtx_p3_max_bytes(dc.image_width, dc.image_height), '\0');
+  size_t len = 0;
+  if (rtx_render_p3(gpu.device_scene(), &dc, &p, bytes.data(), bytes.size(), &len, rgb_.data(), nullptr, &st) != RTX_OK)
+    throw std::runtime_error(std::string("rtx_render_p3: ") + rtx_last_error());
+  out.write(bytes.data(), (std::streamsize)len);
 }
 
 }  // namespace rt::renderer

@@ -102,7 +102,7 @@ EXPORTS = ["rtx_abi_version", "rtx_last_error", "rtx_device_count", "rtx_scene_c
            "rtx_intersect", "rtx_intersect_device", "rtx_camera_init", "rtx_render", "rtx_render_pixel_count",
            "rtx_render_device", "rtx_host_scene_load", "rtx_host_scene_recipe", "rtx_host_scene_write",
            "rtx_host_scene_desc", "rtx_host_scene_prim_indices", "rtx_host_scene_destroy",
-           "rtx_camera_config_load", "rtx_write_ppm"]
+           "rtx_camera_config_load", "rtx_write_ppm", "rtx_p3_max_bytes", "rtx_render_p3", "rtx_encode_p3_device"]
 
 _lib = None
 
@@ -136,6 +136,10 @@ def lib():
             "rtx_host_scene_destroy": ([vp], C.c_int),
             "rtx_camera_config_load": ([C.c_char_p, C.c_char_p, C.POINTER(CameraConfig)], C.c_int),
             "rtx_write_ppm": ([C.c_char_p, vp, i32, i32], C.c_int),
+            "rtx_p3_max_bytes": ([i32, i32], sz),
+            "rtx_render_p3": ([vp, C.POINTER(Camera), C.POINTER(RenderParams), vp, sz, C.POINTER(sz), vp, vp,
+                               C.POINTER(Stats)], C.c_int),
+            "rtx_encode_p3_device": ([vp, vp, i32, i32, vp, sz, C.POINTER(sz), vp], C.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -286,6 +290,31 @@ class DeviceScene:
         _check(lib().rtx_render(self.h, C.byref(cam), C.byref(p), rgb.ctypes.data_as(C.c_void_p),
                                 spp_out.ctypes.data_as(C.c_void_p), C.byref(st)), "rtx_render")
         return rgb, spp_out, st.as_dict()
+
+    def render_p3(self, cam, spp, max_depth, seed=1234, adaptive=True, mode="wavefront", precision="parity",
+                  tile=None):
+        """Render and return the P3 PPM file bytes, encoded on the device (rtx_render_p3)."""
+        p = RenderParams()
+        p.spp, p.max_depth, p.adaptive = spp, max_depth, int(bool(adaptive))
+        p.min_spp, p.rel_threshold, p.seed = 16, float(np.float32(0.05)), seed
+        p.mode, p.precision = MODES[mode], PRECISIONS[precision]
+        if tile is not None:
+            p.x0, p.y0, p.w, p.h = tile
+        cap = lib().rtx_p3_max_bytes(cam.image_width, cam.image_height)
+        buf = C.create_string_buffer(cap)
+        n = C.c_size_t()
+        st = Stats()
+        _check(lib().rtx_render_p3(self.h, C.byref(cam), C.byref(p), buf, cap, C.byref(n), None, None,
+                                   C.byref(st)), "rtx_render_p3")
+        return buf.raw[:n.value], st.as_dict()
+
+    def encode_p3_device(self, d_rgb, width, height, d_out, cap, stream=0):
+        """P3 bytes of a device framebuffer into a device buffer; returns the byte count."""
+        n = C.c_size_t()
+        _check(lib().rtx_encode_p3_device(self.h, C.c_void_p(d_rgb), width, height, C.c_void_p(d_out), cap,
+                                          C.byref(n), C.c_void_p(stream) if stream else None),
+               "rtx_encode_p3_device")
+        return n.value
 
     def render_device(self, cam, params, d_rgb, d_spp=0, stream=0):
         """Device-resident render into caller buffers (e.g. torch tensors' data_ptr())."""

@@ -256,7 +256,22 @@ int rtx_host_scene_destroy(rtx_host_scene* s);
 /* cameras.json preset -> config (parseCamera/loadCameras, scene/camera.h:40-67). */
 int rtx_camera_config_load(const char* json_path, const char* preset, rtx_camera_config* out);
 
-/* write_color bytes (core/color.h:18-33) as a P3 PPM; rgb is a linear framebuffer. */
+/* ---- P3 PPM output encoded on the device (wavefront.cc:238-241 header + write_color,
+ * core/color.h:18-33, per pixel; SURVEY §8f "on-GPU resolve + PPM output").  The bytes are
+ * identical to rtx_write_ppm / the reference's Render() output. */
+/* Upper bound of the P3 file size of a width x height image (header + 12 B per pixel). */
+size_t rtx_p3_max_bytes(int32_t width, int32_t height);
+/* Render like rtx_render and return the P3 file bytes of the rendered pixels (the tile /
+   stripe subset: width x rows) in `out` (host, cap >= rtx_p3_max_bytes); *out_len = bytes.
+   out_rgb (linear framebuffer) and out_spp are optional (NULL). */
+int rtx_render_p3(rtx_scene* scene, const rtx_camera* cam, const rtx_render_params* params, char* out, size_t cap,
+                  size_t* out_len, double* out_rgb, int32_t* out_spp, rtx_stats* stats);
+/* P3 file bytes of a device-resident linear framebuffer (width x height x 3 doubles) into a
+   device buffer d_out (cap >= rtx_p3_max_bytes); synchronizes `stream` to report *out_len. */
+int rtx_encode_p3_device(rtx_scene* scene, const double* d_rgb, int32_t width, int32_t height, char* d_out,
+                         size_t cap, size_t* out_len, void* stream);
+
+/* write_color bytes (core/color.h:18-33) as a P3 PPM; rgb is a linear framebuffer (host). */
 int rtx_write_ppm(const char* path, const double* rgb, int32_t width, int32_t height);
 
 #ifdef __cplusplus
