@@ -176,6 +176,10 @@ struct BvhNodeGPU {
   uint32_t isLeaf;
 };
 
+// The binned-SAH build over primitive boxes (bvh.h:166-367): nodes in pre-order and the
+// leaf-order permutation.  Bvh::Build and rtx_bvh_build_host use it.
+void BuildSah(const std::vector<Aabb>& bounds, std::vector<int>& prim_indices, std::vector<BvhNodeGPU>& nodes);
+
 class Bvh : public Hittable {
  public:
   explicit Bvh(scene::Scene& scene);

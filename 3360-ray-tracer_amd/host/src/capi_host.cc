@@ -1,5 +1,6 @@
 // capi_host.cc — the host-side part of include/rtx.h: scene assembly helpers and
 // cameras.json presets, implemented with the C++ host API (rt::scene / rt::geom).
+#include <cmath>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -75,6 +76,67 @@ int rtx_host_scene_prim_indices(const rtx_host_scene* s, int32_t* out, int64_t n
   if (!s || !out) return host_fail(RTX_ERR_INVALID, "NULL argument");
   if (n != (int64_t)s->flat.prim_indices.size()) return host_fail(RTX_ERR_INVALID, "n != number of prim indices");
   std::memcpy(out, s->flat.prim_indices.data(), n * sizeof(int32_t));
+  return RTX_OK;
+}
+
+// Hittable::BoundingBox of each primitive record, as the host classes compute it
+// (sphere.h, triangle.h:18-38, rect.h:42-45,87-89,132-134): the SAH builder's input.
+int rtx_prim_bounds(const rtx_prim* prims, int64_t n, double* out) {
+  if ((!prims || !out) && n > 0) return host_fail(RTX_ERR_INVALID, "NULL argument");
+  using rt::core::Point3;
+  using rt::core::Vec3;
+  for (int64_t i = 0; i < n; i++) {
+    const rtx_prim& p = prims[i];
+    const double* g = p.g;
+    rt::geom::Aabb b;
+    if (p.kind == RTX_PRIM_SPHERE) {
+      const Vec3 rv(g[3], g[3], g[3]);
+      const Point3 c(g[0], g[1], g[2]);
+      b = rt::geom::Aabb(Point3(c + rv), Point3(c - rv));
+    } else if (p.kind == RTX_PRIM_TRIANGLE) {
+      Point3 mn(std::fmin(g[0], std::fmin(g[3], g[6])), std::fmin(g[1], std::fmin(g[4], g[7])),
+                std::fmin(g[2], std::fmin(g[5], g[8])));
+      Point3 mx(std::fmax(g[0], std::fmax(g[3], g[6])), std::fmax(g[1], std::fmax(g[4], g[7])),
+                std::fmax(g[2], std::fmax(g[5], g[8])));
+      const double eps = 1e-6f;
+      mn += -Vec3(eps, eps, eps);
+      mx += Vec3(eps, eps, eps);
+      b = rt::geom::Aabb(mn, mx);
+    } else if (p.kind >= RTX_PRIM_XY_RECT && p.kind <= RTX_PRIM_YZ_RECT) {
+      rt::geom::AxisRect r(p.kind, g[0], g[1], g[2], g[3], g[4], nullptr);
+      b = r.BoundingBox();
+    } else {
+      return host_fail(RTX_ERR_INVALID, "unknown primitive kind");
+    }
+    const double v[6] = {b.x.min_, b.y.min_, b.z.min_, b.x.max_, b.y.max_, b.z.max_};
+    std::memcpy(out + 6 * i, v, sizeof v);
+  }
+  return RTX_OK;
+}
+
+int rtx_bvh_build_host(const double* bounds, int64_t n, rtx_bvh_node* out_nodes, int64_t* out_n_nodes,
+                       uint32_t* out_prim_indices) {
+  if ((!bounds && n > 0) || !out_nodes || !out_n_nodes || !out_prim_indices)
+    return host_fail(RTX_ERR_INVALID, "NULL argument");
+  if (n < 0 || n > 0x3FFFFFFF) return host_fail(RTX_ERR_INVALID, "primitive count out of range");
+  std::vector<rt::geom::Aabb> b(n);
+  for (int64_t i = 0; i < n; i++) {
+    const double* q = bounds + 6 * i;
+    b[i] = rt::geom::Aabb(rt::core::Interval(q[0], q[3]), rt::core::Interval(q[1], q[4]),
+                          rt::core::Interval(q[2], q[5]));
+  }
+  std::vector<int> idx;
+  std::vector<rt::geom::BvhNodeGPU> nodes;
+  rt::geom::BuildSah(b, idx, nodes);
+  for (size_t i = 0; i < nodes.size(); i++) {
+    rtx_bvh_node& o = out_nodes[i];
+    const rt::geom::Aabb& a = nodes[i].bbox;
+    o.lo[0] = a.x.min_, o.lo[1] = a.y.min_, o.lo[2] = a.z.min_;
+    o.hi[0] = a.x.max_, o.hi[1] = a.y.max_, o.hi[2] = a.z.max_;
+    o.left_first = nodes[i].left_pIdx, o.right_count = nodes[i].right_pCnt, o.is_leaf = nodes[i].isLeaf, o.pad_ = 0;
+  }
+  for (int64_t i = 0; i < n; i++) out_prim_indices[i] = (uint32_t)idx[i];
+  *out_n_nodes = (int64_t)nodes.size();
   return RTX_OK;
 }
 

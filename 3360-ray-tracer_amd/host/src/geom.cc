@@ -164,20 +164,25 @@ Bvh::Bvh(scene::Scene& scene) : Bvh(scene.objects_) {}
 
 Bvh::Bvh(std::vector<std::shared_ptr<Hittable>>& objects) : primitives_(objects) { Build(); }
 
-void Bvh::Build() {
-  const int n = (int)primitives_.size();
-  prim_indices_.resize(n);
-  nodes_.clear();
+void BuildSah(const std::vector<Aabb>& bounds, std::vector<int>& prim_indices, std::vector<BvhNodeGPU>& nodes) {
+  const int n = (int)bounds.size();
+  prim_indices.resize(n);
+  nodes.clear();
   if (n == 0) return;
-  SahBuilder b{prim_indices_, {}, {}, nodes_};
-  b.bounds.resize(n), b.centroids.resize(n);
+  SahBuilder b{prim_indices, bounds, {}, nodes};
+  b.centroids.resize(n);
   for (int i = 0; i < n; i++) {
-    prim_indices_[i] = i;
-    b.bounds[i] = primitives_[i]->BoundingBox();
+    prim_indices[i] = i;
     b.centroids[i] = b.bounds[i].center();
   }
-  nodes_.reserve(2 * (size_t)n);
+  nodes.reserve(2 * (size_t)n);
   b.Emit(0, n);
+}
+
+void Bvh::Build() {
+  std::vector<Aabb> bounds(primitives_.size());
+  for (size_t i = 0; i < primitives_.size(); i++) bounds[i] = primitives_[i]->BoundingBox();
+  BuildSah(bounds, prim_indices_, nodes_);
 }
 
 Mesh::Mesh(const std::vector<core::Point3>& v, const std::vector<std::array<int, 3>>& f,

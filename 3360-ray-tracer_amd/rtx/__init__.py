@@ -102,7 +102,8 @@ EXPORTS = ["rtx_abi_version", "rtx_last_error", "rtx_device_count", "rtx_scene_c
            "rtx_intersect", "rtx_intersect_device", "rtx_camera_init", "rtx_render", "rtx_render_pixel_count",
            "rtx_render_device", "rtx_host_scene_load", "rtx_host_scene_recipe", "rtx_host_scene_write",
            "rtx_host_scene_desc", "rtx_host_scene_prim_indices", "rtx_host_scene_destroy",
-           "rtx_camera_config_load", "rtx_write_ppm", "rtx_p3_max_bytes", "rtx_render_p3", "rtx_encode_p3_device"]
+           "rtx_camera_config_load", "rtx_write_ppm", "rtx_p3_max_bytes", "rtx_render_p3", "rtx_encode_p3_device",
+           "rtx_prim_bounds", "rtx_bvh_build", "rtx_bvh_build_host"]
 
 _lib = None
 
@@ -140,6 +141,9 @@ def lib():
             "rtx_render_p3": ([vp, C.POINTER(Camera), C.POINTER(RenderParams), vp, sz, C.POINTER(sz), vp, vp,
                                C.POINTER(Stats)], C.c_int),
             "rtx_encode_p3_device": ([vp, vp, i32, i32, vp, sz, C.POINTER(sz), vp], C.c_int),
+            "rtx_prim_bounds": ([vp, i64, vp], C.c_int),
+            "rtx_bvh_build": ([C.c_int, vp, i64, vp, C.POINTER(i64), vp], C.c_int),
+            "rtx_bvh_build_host": ([vp, i64, vp, C.POINTER(i64), vp], C.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -323,6 +327,31 @@ class DeviceScene:
                                        C.c_void_p(d_spp) if d_spp else None, C.byref(st),
                                        C.c_void_p(stream) if stream else None), "rtx_render_device")
         return st.as_dict()
+
+
+def prim_bounds(prims):
+    """Reference BoundingBox of each primitive record (PRIM_DTYPE array) -> (n, 6) float64."""
+    prims = np.ascontiguousarray(prims)
+    out = np.zeros((len(prims), 6))
+    _check(lib().rtx_prim_bounds(prims.ctypes.data_as(C.c_void_p), len(prims), out.ctypes.data_as(C.c_void_p)),
+           "rtx_prim_bounds")
+    return out
+
+
+def bvh_build(bounds, device=0, on="gpu"):
+    """Binned-SAH BVH over (n, 6) primitive boxes: (nodes NODE_DTYPE, prim_indices uint32).
+    on="gpu": rtx_bvh_build (device); on="host": rtx_bvh_build_host (the C++ builder)."""
+    bounds = np.ascontiguousarray(bounds, dtype=np.float64).reshape(-1, 6)
+    n = len(bounds)
+    nodes = np.zeros(max(1, 2 * n), NODE_DTYPE)
+    idx = np.zeros(max(1, n), np.uint32)
+    nn = C.c_int64()
+    bp, np_, ip = bounds.ctypes.data_as(C.c_void_p), nodes.ctypes.data_as(C.c_void_p), idx.ctypes.data_as(C.c_void_p)
+    if on == "gpu":
+        _check(lib().rtx_bvh_build(device, bp, n, np_, C.byref(nn), ip), "rtx_bvh_build")
+    else:
+        _check(lib().rtx_bvh_build_host(bp, n, np_, C.byref(nn), ip), "rtx_bvh_build_host")
+    return nodes[:nn.value], idx[:n]
 
 
 def stripe_rows_of(height, stripe_rows, index, count):

@@ -256,6 +256,19 @@ int rtx_host_scene_destroy(rtx_host_scene* s);
 /* cameras.json preset -> config (parseCamera/loadCameras, scene/camera.h:40-67). */
 int rtx_camera_config_load(const char* json_path, const char* preset, rtx_camera_config* out);
 
+/* ---- BVH build (SURVEY §8f "GPU BVH build"; bvh.h:39-68,166-367) -------------------- */
+/* Reference BoundingBox of each primitive (n x 6 doubles: lo xyz, hi xyz), host-side. */
+int rtx_prim_bounds(const rtx_prim* prims, int64_t n, double* out_bounds);
+/* Binned-SAH BVH over n primitive boxes (in the primitives' original order), built on the
+   GPU.  Output is byte-identical to the host builder's (= the reference's Bvh::Build):
+   out_nodes (capacity 2n) in pre-order, *out_n_nodes, out_prim_indices[n] (the permutation:
+   leaf slot -> original primitive).  Host buffers; the device work is internal. */
+int rtx_bvh_build(int device, const double* bounds, int64_t n, rtx_bvh_node* out_nodes, int64_t* out_n_nodes,
+                  uint32_t* out_prim_indices);
+/* The same build on the host (the C++ builder scene assembly uses); identical outputs. */
+int rtx_bvh_build_host(const double* bounds, int64_t n, rtx_bvh_node* out_nodes, int64_t* out_n_nodes,
+                       uint32_t* out_prim_indices);
+
 /* ---- P3 PPM output encoded on the device (wavefront.cc:238-241 header + write_color,
  * core/color.h:18-33, per pixel; SURVEY §8f "on-GPU resolve + PPM output").  The bytes are
  * identical to rtx_write_ppm / the reference's Render() output. */
