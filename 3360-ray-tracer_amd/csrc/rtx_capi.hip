@@ -627,8 +627,10 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
   if (!sc || !cam || !prm || !d_rgb) return fail(RTX_ERR_INVALID, "NULL argument");
   if (prm->spp < 0 || prm->max_depth < 0) return fail(RTX_ERR_INVALID, "negative spp / max_depth");
   if (prm->mode < RTX_MODE_WAVEFRONT || prm->mode > RTX_MODE_MEGAKERNEL) return fail(RTX_ERR_INVALID, "bad mode");
-  if (prm->adaptive && prm->mode == RTX_MODE_MEGAKERNEL)
-    return fail(RTX_ERR_INVALID, "adaptive sampling is a WavefrontRenderer feature (use AdaptiveSampler semantics: not provided)");
+  // MegaKernel + adaptive = AdaptiveSampler(min_spp, spp, rel_threshold): up to spp + 1 samples
+  const bool mk_adaptive = prm->adaptive && prm->mode == RTX_MODE_MEGAKERNEL;
+  if (mk_adaptive && prm->spp >= 0x7FFFFFFF) return fail(RTX_ERR_INVALID, "spp too large");
+  const int budget = mk_adaptive ? prm->spp + 1 : prm->spp;
   PixelMap map;
   std::string err;
   const int64_t npix = subset_pixels(cam, prm, map, err);
@@ -642,9 +644,9 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
   int K = prm->samples_per_group;
   if (K <= 0) {
     const int64_t target = 1ll << 25;
-    K = (int)std::max<int64_t>(1, std::min<int64_t>(prm->spp > 0 ? prm->spp : 1, target / std::max<int64_t>(1, npix)));
+    K = (int)std::max<int64_t>(1, std::min<int64_t>(budget > 0 ? budget : 1, target / std::max<int64_t>(1, npix)));
   }
-  K = std::max(1, std::min(K, std::max(1, prm->spp)));
+  K = std::max(1, std::min(K, std::max(1, budget)));
   if ((int64_t)npix * K > 0xFFFFFFFFll) return fail(RTX_ERR_INVALID, "too many slots in one group (lower samples_per_group)");
   const int64_t nslots = npix * (int64_t)K;
 
@@ -710,8 +712,8 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
   if (timed) HIPC(hipEventRecord(sc->ev[0], s));
   const int pix_blocks = (int)((npix + kBlock - 1) / kBlock);
   const int wf_grid = std::max(1, std::min<int>(sc->cus * 16, (int)((nslots + kBlock - 1) / kBlock)));
-  for (int s0 = 0, Kc = 0; s0 < prm->spp; s0 += Kc) {
-    Kc = std::min(K, prm->spp - s0);
+  for (int s0 = 0, Kc = 0; s0 < budget; s0 += Kc) {
+    Kc = std::min(K, budget - s0);
     // adaptive with automatic grouping: nothing can converge before min_spp, afterwards
     // small groups limit the samples traced past a pixel's convergence point
     if (prm->adaptive && prm->samples_per_group <= 0)
@@ -759,15 +761,18 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
         hot_ms += ms;
       }
     }
-    if (prm->mode == RTX_MODE_MEGAKERNEL)
+    if (mk_adaptive)
+      hipLaunchKernelGGL(k_accumulate_mk_adaptive, dim3(pix_blocks), dim3(kBlock), 0, s, px, A.L, npix, Kc,
+                         prm->min_spp, prm->spp, prm->rel_threshold);
+    else if (prm->mode == RTX_MODE_MEGAKERNEL)
       hipLaunchKernelGGL(k_accumulate_sum, dim3(pix_blocks), dim3(kBlock), 0, s, px, A.L, npix, Kc);
     else
       hipLaunchKernelGGL(k_accumulate, dim3(pix_blocks), dim3(kBlock), 0, s, px, A.L, npix, Kc, prm->adaptive,
                          prm->min_spp, prm->rel_threshold);
     HIPC(hipGetLastError());
   }
-  hipLaunchKernelGGL(k_resolve, dim3(pix_blocks), dim3(kBlock), 0, s, px, npix, prm->mode == RTX_MODE_MEGAKERNEL,
-                     prm->spp, d_rgb, d_spp);
+  hipLaunchKernelGGL(k_resolve, dim3(pix_blocks), dim3(kBlock), 0, s, px, npix,
+                     prm->mode == RTX_MODE_MEGAKERNEL ? (mk_adaptive ? 2 : 1) : 0, prm->spp, d_rgb, d_spp);
   HIPC(hipGetLastError());
   if (timed) {
     HIPC(hipEventRecord(sc->ev[1], s));

@@ -427,18 +427,67 @@ __global__ __launch_bounds__(kBlock) void k_accumulate_sum(PixelSoA px, const do
   px.samples[p] += K;
 }
 
+// AdaptiveSampler::SamplePixel (sampler.h:44-82) replayed in sample order for the MegaKernel
+// renderer.  Its quirks are kept: `pixel` is the running SUM of the samples and the mean /
+// variance are taken over those running sums; luminance uses float weights (color.h:35-37);
+// the loop runs while samples <= max_samples, i.e. up to max_samples + 1 samples.  State:
+// px.sum = pixel, px.mean = sum, px.m2 = sum_sq, px.samples, px.conv = finished.
+__device__ __forceinline__ double luminance(double x, double y, double z) {
+  return (double)0.2126f * x + (double)0.7152f * y + (double)0.0722f * z;
+}
+__global__ __launch_bounds__(kBlock) void k_accumulate_mk_adaptive(PixelSoA px, const double* __restrict__ L,
+                                                                   int64_t npix, int K, int min_samples,
+                                                                   int max_samples, double threshold) {
+  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (p >= npix) return;
+  if (px.conv[p]) return;
+  double pixel[3], sum[3], sq[3];
+  for (int c = 0; c < 3; c++)
+    pixel[c] = px.sum[c * npix + p], sum[c] = px.mean[c * npix + p], sq[c] = px.m2[c * npix + p];
+  int n = px.samples[p];
+  bool done = false;
+  for (int k = 0; k < K && !done; k++) {
+    if (n > max_samples) {  // while (samples <= max_samples_) fails
+      done = true;
+      break;
+    }
+    n++;
+    const double* x = L + 3 * (p * K + k);
+    for (int c = 0; c < 3; c++) pixel[c] += x[c];
+    for (int c = 0; c < 3; c++) sum[c] += pixel[c];
+    for (int c = 0; c < 3; c++) sq[c] += pixel[c] * pixel[c];
+    if (n >= min_samples) {
+      const double inv = 1.0 / n;  // Vec3 / int is (1/t) * v
+      double mean[3], var[3];
+      for (int c = 0; c < 3; c++) mean[c] = inv * sum[c];
+      const double mean_lum = luminance(mean[0], mean[1], mean[2]);
+      for (int c = 0; c < 3; c++) var[c] = inv * sq[c] - mean[c] * mean[c];
+      const double error = sqrt(luminance(var[0], var[1], var[2]) / n);
+      if ((error / (mean_lum + (double)1e-3f)) < threshold) done = true;
+    }
+  }
+  if (n > max_samples) done = true;
+  for (int c = 0; c < 3; c++)
+    px.sum[c * npix + p] = pixel[c], px.mean[c * npix + p] = sum[c], px.m2[c * npix + p] = sq[c];
+  px.samples[p] = n;
+  px.conv[p] = done ? 1 : 0;
+}
+
 // wavefront.cc:229-235: sum / (float)samples  (Vec3 operator/ is (1/t)*v); megakernel
-// (mega_kernel.h + sampler.h:32): pixel /= num_samples.
+// (mega_kernel.h + sampler.h:32,79): pixel /= num_samples (DefaultSampler) or /= samples
+// (AdaptiveSampler).
 __global__ __launch_bounds__(kBlock) void k_resolve(PixelSoA px, int64_t npix, int megakernel, int spp,
                                                     double* __restrict__ rgb, int32_t* __restrict__ spp_out) {
+  // megakernel: 1 = DefaultSampler (divide by spp), 2 = AdaptiveSampler (by the pixel's count)
   const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (p >= npix) return;
   const int n = px.samples[p];
   double s = 0.0;
-  if (megakernel) s = 1.0 / (double)spp;
+  if (megakernel == 1) s = 1.0 / (double)spp;
+  else if (megakernel == 2) s = 1.0 / (double)n;
   else if (n > 0) s = 1.0 / (double)(float)n;
   for (int c = 0; c < 3; c++) rgb[3 * p + c] = (megakernel || n > 0) ? s * px.sum[c * npix + p] : 0.0;
-  if (spp_out) spp_out[p] = megakernel ? spp : n;
+  if (spp_out) spp_out[p] = megakernel == 1 ? spp : n;
 }
 
 }  // namespace rtxd

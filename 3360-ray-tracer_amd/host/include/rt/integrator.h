@@ -68,5 +68,19 @@ class DefaultSampler : public Sampler {  // sampler.h:22-37
  private:
   int n_;
 };
+// sampler.h:44-82: per pixel until the relative error of the running sums drops below
+// `threshold` (after min_samples), at most max_samples + 1 samples.
+class AdaptiveSampler : public Sampler {
+ public:
+  AdaptiveSampler(int min_samples, int max_samples, float threshold)
+      : min_samples_(min_samples), max_samples_(max_samples), threshold_(threshold) {}
+  int num_samples() const override { return max_samples_; }
+  int min_samples() const { return min_samples_; }
+  float threshold() const { return threshold_; }
+
+ private:
+  int min_samples_, max_samples_;
+  float threshold_;
+};
 
 }  // namespace rt::integrator

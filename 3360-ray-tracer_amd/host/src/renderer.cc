@@ -104,6 +104,11 @@ void MegaKernel::Render(std::ostream& out) {
   const rtx_camera& dc = cam_.device();
   rtx_render_params p = DefaultParams(sampler_.num_samples(), cam_.max_depth_);
   p.adaptive = 0;
+  if (auto* a = dynamic_cast<const integrator::AdaptiveSampler*>(&sampler_)) {
+    p.adaptive = 1;
+    p.min_spp = a->min_samples();
+    p.rel_threshold = (double)a->threshold();
+  }
   p.mode = RTX_MODE_MEGAKERNEL;
   p.seed = seed_;
   rtx_stats st{};

@@ -1,7 +1,10 @@
 // raytracer — CLI drop-in for the reference binary (main.cc:158-197):
 //   raytracer [camera-preset] [--scene cornell|three|final|bunny|mixed|<file.rtxs>]
 //             [--cameras cameras.json] [--spp N] [--depth N] [--seed S] [--fixed]
-//             [--mode wavefront|persistent|megakernel] [--precision parity|fast] > out.ppm
+//             [--mode wavefront|persistent|megakernel] [--precision parity|fast]
+//             [--mk-adaptive MIN:THRESHOLD] > out.ppm
+// --mk-adaptive selects the AdaptiveSampler (sampler.h:44-82) for --mode megakernel,
+// with max_samples = the preset's (or --spp) samples.
 // Defaults follow main.cc: preset "default" (fallback when unknown), the Cornell box
 // scene (switch(4), main.cc:178-183), WavefrontRenderer with the preset's maxDepth and
 // samplesPerPixel, adaptive sampling on; "Runtime: Xs" on stderr.
@@ -23,6 +26,8 @@ int main(int argc, char** argv) {
   int spp = -1, depth = -1;
   uint64_t seed = 1234;
   bool fixed = false;
+  int mk_min = -1;
+  float mk_thr = 0.0f;
   for (int i = 1; i < argc; i++) {
     std::string a = argv[i];
     auto next = [&]() -> std::string {
@@ -40,6 +45,16 @@ int main(int argc, char** argv) {
     else if (a == "--mode") mode = next();
     else if (a == "--precision") precision = next();
     else if (a == "--fixed") fixed = true;
+    else if (a == "--mk-adaptive") {
+      const std::string v = next();
+      const size_t c = v.find(':');
+      if (c == std::string::npos) {
+        std::cerr << "--mk-adaptive expects MIN:THRESHOLD\n";
+        return 2;
+      }
+      mk_min = std::atoi(v.substr(0, c).c_str());
+      mk_thr = std::strtof(v.substr(c + 1).c_str(), nullptr);
+    }
     else if (!a.empty() && a[0] != '-') preset = a;
     else {
       std::cerr << "unknown option " << a << "\n";
@@ -67,7 +82,9 @@ int main(int argc, char** argv) {
     const int ns = spp > 0 ? spp : cam.samples_per_pixel_;
     const int md = depth >= 0 ? depth : cam.max_depth_;
     if (mode == "megakernel") {
-      integrator::DefaultSampler sampler(ns);
+      integrator::DefaultSampler fixed_sampler(ns);
+      integrator::AdaptiveSampler adaptive_sampler(mk_min, ns, mk_thr);
+      integrator::Sampler& sampler = mk_min >= 0 ? (integrator::Sampler&)adaptive_sampler : fixed_sampler;
       cam.max_depth_ = md;
       renderer::MegaKernel r(*world, cam, sampler);
       r.set_seed(seed);

@@ -177,9 +177,12 @@ enum {
 typedef struct {
   int32_t spp;              /* max_samples (passes) */
   int32_t max_depth;
-  int32_t adaptive;         /* 1: reference adaptive sampling (pixel_state.h:54-72) */
-  int32_t min_spp;          /* adaptive: kMinSamples (wavefront.cc:43) = 16 */
-  double rel_threshold;     /* adaptive: kRelThresh (float 0.05, wavefront.cc:42) */
+  int32_t adaptive;         /* 1: adaptive sampling.  WAVEFRONT/PERSISTENT: the renderer's
+                               PixelState test (pixel_state.h:54-72); MEGAKERNEL:
+                               AdaptiveSampler(min_spp, spp, rel_threshold) (sampler.h:44-82,
+                               up to spp + 1 samples); 0: fixed spp / DefaultSampler */
+  int32_t min_spp;          /* adaptive: kMinSamples (wavefront.cc:43) = 16 | min_samples_ */
+  double rel_threshold;     /* adaptive: kRelThresh (float 0.05, wavefront.cc:42) | threshold_ */
   uint64_t seed;            /* Philox key: results depend on (seed, pixel, sample) only */
   int32_t mode;             /* RTX_MODE_* */
   int32_t precision;        /* RTX_PREC_* */

@@ -73,6 +73,11 @@ MEGA_CASES = [
     ("mega_cornell", "cornell", "cornell", 24, 4, 10, 29, {}),
     ("mega_final", "final", "c2_final", 32, 2, 50, 31, {}),
 ]
+# MegaKernel + AdaptiveSampler(min, max, threshold): (name, scene, preset, width, depth, min, max, thr, seed)
+MEGA_ADAPTIVE_CASES = [
+    ("mega_adaptive_three", "three", "c1_three", 24, 10, 4, 24, 0.05, 37),
+    ("mega_adaptive_final", "final", "c2_final", 24, 50, 8, 32, 0.02, 41),
+]
 
 
 def rays_for(scene, rng, n):
@@ -265,6 +270,19 @@ def main():
         np.savez_compressed(os.path.join(GOLD, "render_" + name + ".npz"), fb=fb, ppm=np.frombuffer(ppm, dtype=np.uint8))
         manifest[name] = {"scene": scene, "camera": cfg, "width": w, "spp": spp, "max_depth": depth,
                           "seed": seed, "mode": "megakernel"}
+    for name, scene, preset, w, depth, mn, mx, thr, seed in MEGA_ADAPTIVE_CASES:
+        cfg = dict(cams[preset])
+        pre = os.path.join(tmp, name)
+        run("megakernel_adaptive", os.path.join(tmp, scene + ".rtxs"), ASSETS, *cam_args(cfg, w), depth, mn, mx,
+            repr(thr), seed, pre)
+        fb = np.fromfile(pre + ".f64", dtype=np.float64)
+        sp = np.fromfile(pre + ".spp", dtype=np.int32)
+        ppm = open(pre + ".ppm", "rb").read()
+        np.savez_compressed(os.path.join(GOLD, "render_" + name + ".npz"), fb=fb, spp=sp,
+                            ppm=np.frombuffer(ppm, dtype=np.uint8))
+        manifest[name] = {"scene": scene, "camera": cfg, "width": w, "spp": mx, "max_depth": depth, "seed": seed,
+                          "mode": "megakernel", "adaptive": 1, "min_samples": mn,
+                          "threshold": float(np.float32(thr))}
     meta["renders"] = manifest
     json.dump(meta, open(os.path.join(GOLD, "manifest.json"), "w"), indent=1, sort_keys=True)
     shutil.rmtree(tmp)

@@ -624,6 +624,48 @@ void render_megakernel(RefScene& S, Cam& cam, int max_depth, int spp, const std:
   write_bin(out + ".f64", fb);
 }
 
+// MegaKernel with AdaptiveSampler::SamplePixel (sampler.h:44-82), single-threaded,
+// row-major.  sampler.h needs scene/camera.h (nlohmann/json, absent), so its loop is
+// restated here over the reference's own GetRay / Hit / Scatter / Color / luminance.
+void render_megakernel_adaptive(RefScene& S, Cam& cam, int max_depth, int min_samples, int max_samples,
+                                float threshold, const std::string& out) {
+  const int W = cam.image_width, H = cam.image_height;
+  std::vector<double> fb(3 * (size_t)W * H);
+  std::vector<int32_t> spp((size_t)W * H);
+  std::ofstream ppm(out + ".ppm");
+  ppm << "P3\n" << W << ' ' << H << "\n255\n";
+  for (int y = 0; y < H; y++)
+    for (int x = 0; x < W; x++) {
+      Color pixel(0, 0, 0);
+      Color sum = Color(0, 0, 0);
+      Color sum_sq = Color(0, 0, 0);
+      int samples = 0;
+      while (samples <= max_samples) {
+        samples++;
+        core::Ray r = cam.GetRay(x, y);
+        pixel += get_pixel(r, max_depth, S.world);
+        sum += pixel;
+        sum_sq += pixel * pixel;
+        if (samples >= min_samples) {
+          Color mean = sum / samples;
+          double mean_luminance = core::luminance(mean);
+          Color variance = (sum_sq / samples) - (mean * mean);
+          double error = sqrt(core::luminance(variance) / samples);
+          if ((error / (mean_luminance + 1e-3f)) < threshold) break;
+        }
+      }
+      pixel /= samples;
+      size_t i = (size_t)y * W + x;
+      fb[3 * i] = pixel.x();
+      fb[3 * i + 1] = pixel.y();
+      fb[3 * i + 2] = pixel.z();
+      spp[i] = samples;
+      core::write_color(ppm, pixel);
+    }
+  write_bin(out + ".f64", fb);
+  write_bin(out + ".spp", spp);
+}
+
 void usage() {
   std::fprintf(stderr,
                "ref_harness recipe <name> <out.rtxs>\n"
@@ -639,7 +681,9 @@ void usage() {
                "ref_harness render <scene.rtxs> <model_dir> <cam 14 numbers> <maxdepth> <spp> <adaptive> "
                "<seed> <out_prefix>\n"
                "ref_harness megakernel <scene.rtxs> <model_dir> <cam 14 numbers> <maxdepth> <spp> <seed> "
-               "<out_prefix>\n");
+               "<out_prefix>\n"
+               "ref_harness megakernel_adaptive <scene.rtxs> <model_dir> <cam 14 numbers> <maxdepth> <min> <max> "
+               "<threshold> <seed> <out_prefix>\n");
   std::exit(2);
 }
 
@@ -835,6 +879,12 @@ int main(int argc, char** argv) {
     Cam cam = parse_cam(argv + 4);
     core::SeedRng((unsigned)std::strtoul(argv[20], nullptr, 10));
     render_megakernel(*S, cam, std::atoi(argv[18]), std::atoi(argv[19]), argv[21]);
+  } else if (cmd == "megakernel_adaptive" && argc == 24) {
+    auto S = load_scene(argv[2], argv[3]);
+    Cam cam = parse_cam(argv + 4);
+    core::SeedRng((unsigned)std::strtoul(argv[22], nullptr, 10));
+    render_megakernel_adaptive(*S, cam, std::atoi(argv[18]), std::atoi(argv[19]), std::atoi(argv[20]),
+                               std::strtof(argv[21], nullptr), argv[23]);
   } else {
     usage();
   }

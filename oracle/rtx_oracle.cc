@@ -795,6 +795,8 @@ struct Params {
   uint64_t seed = 1234;
   int x0 = 0, y0 = 0, w = 0, h = 0;  // tile (philox mode); mt mode renders the whole image
   int threads = 1;
+  int mk_min_samples = 0;      // megakernel AdaptiveSampler (adaptive = 1)
+  double mk_threshold = 0.0;
 };
 
 struct Stats {
@@ -965,7 +967,11 @@ V3 get_pixel(const Scene& S, V3 o, V3 d, int depth, int max_depth, Rng& g, long 
   return sky(d);
 }
 
-void render_megakernel(const Scene& S, const Camera& cam, const Params& P, double* fb, Stats& st) {
+inline double luminance(V3 c) {  // color.h:35-37 (float weights)
+  return 0.2126f * c.x + 0.7152f * c.y + 0.0722f * c.z;
+}
+
+void render_megakernel(const Scene& S, const Camera& cam, const Params& P, double* fb, int* spp_out, Stats& st) {
   const int W = cam.width;
   const bool mt_mode = P.rng_mode == 0;
   std::mt19937 mt(P.seed);
@@ -980,15 +986,39 @@ void render_megakernel(const Scene& S, const Camera& cam, const Params& P, doubl
       Rng g;
       g.mode = P.rng_mode, g.mt = &mt, g.dist = &dist, g.seed = P.seed, g.pixel = y * W + x;
       V3 pixel{0, 0, 0};
-      for (int k = 0; k < P.spp; k++) {
-        g.sample = k, g.open(0);
-        V3 o, d;
-        cam.get_ray(x, y, g, o, d);
-        pixel = pixel + get_pixel(S, o, d, P.max_depth, P.max_depth, g, rays);
+      int samples = 0;
+      if (!P.adaptive) {  // DefaultSampler::SamplePixel (sampler.h:22-34)
+        for (int k = 0; k < P.spp; k++) {
+          g.sample = k, g.open(0);
+          V3 o, d;
+          cam.get_ray(x, y, g, o, d);
+          pixel = pixel + get_pixel(S, o, d, P.max_depth, P.max_depth, g, rays);
+        }
+        pixel = pixel / P.spp;
+        samples = P.spp;
+      } else {  // AdaptiveSampler::SamplePixel (sampler.h:44-82): `pixel` is the running sum
+        V3 sum{0, 0, 0}, sum_sq{0, 0, 0};
+        while (samples <= P.spp) {
+          g.sample = samples, g.open(0);
+          samples++;
+          V3 o, d;
+          cam.get_ray(x, y, g, o, d);
+          pixel = pixel + get_pixel(S, o, d, P.max_depth, P.max_depth, g, rays);
+          sum = sum + pixel;
+          sum_sq = sum_sq + pixel * pixel;
+          if (samples >= P.mk_min_samples) {
+            V3 mean = sum / samples;
+            double mean_luminance = luminance(mean);
+            V3 variance = (sum_sq / samples) - (mean * mean);
+            double error = std::sqrt(luminance(variance) / samples);
+            if ((error / (mean_luminance + 1e-3f)) < P.mk_threshold) break;
+          }
+        }
+        pixel = pixel / samples;
       }
-      pixel = pixel / P.spp;
       size_t oi = (size_t)ty * tw + tx;
       fb[3 * oi] = pixel.x, fb[3 * oi + 1] = pixel.y, fb[3 * oi + 2] = pixel.z;
+      if (spp_out) spp_out[oi] = samples;
     }
   st.rays += rays;
 }
@@ -1152,6 +1182,9 @@ struct orc_params {
   int x0, y0, w, h;  // tile (philox per-pixel / megakernel-philox)
   int threads;
   int mode;  // 0 = wavefront (queue order), 1 = per-pixel (philox), 2 = megakernel
+  // megakernel + adaptive: AdaptiveSampler(min_samples, max_samples = spp, threshold)
+  int mk_min_samples;
+  double mk_threshold;  // the float threshold, widened
 };
 
 static thread_local std::string g_err;
@@ -1327,7 +1360,10 @@ int orc_render(void* sp, orc_camera* c, const orc_params* p, double* fb, int* sp
       return -1;
     }
     render_per_pixel(*s, cam, P, fb, spp, st);
-  } else render_megakernel(*s, cam, P, fb, st);
+  } else {
+    P.mk_min_samples = p->mk_min_samples, P.mk_threshold = p->mk_threshold;
+    render_megakernel(*s, cam, P, fb, spp, st);
+  }
   stats[0] = st.rays, stats[1] = st.primaries;
   return 0;
 }

@@ -25,7 +25,7 @@ class OrcCamera(C.Structure):
 class OrcParams(C.Structure):
     _fields_ = [("spp", C.c_int), ("max_depth", C.c_int), ("adaptive", C.c_int), ("rng_mode", C.c_int),
                 ("seed", C.c_ulonglong), ("x0", C.c_int), ("y0", C.c_int), ("w", C.c_int), ("h", C.c_int),
-                ("threads", C.c_int), ("mode", C.c_int)]
+                ("threads", C.c_int), ("mode", C.c_int), ("mk_min_samples", C.c_int), ("mk_threshold", C.c_double)]
 
 
 _lib = None
@@ -116,10 +116,13 @@ class Scene:
         return out
 
     def render(self, cam_cfg, width, spp, max_depth, seed, adaptive=1, rng="philox", mode="per_pixel",
-               tile=None, threads=1):
+               tile=None, threads=1, mk_min_samples=0, mk_threshold=0.0):
+        """mode="megakernel": adaptive=0 is DefaultSampler(spp); adaptive=1 is
+        AdaptiveSampler(mk_min_samples, spp, mk_threshold) (sampler.h:44-82)."""
         cam = make_camera(cam_cfg, width)
         p = OrcParams()
         p.spp, p.max_depth, p.adaptive = spp, max_depth, adaptive
+        p.mk_min_samples, p.mk_threshold = mk_min_samples, mk_threshold
         p.rng_mode = 0 if rng == "mt" else 1
         p.seed = seed
         p.threads = threads

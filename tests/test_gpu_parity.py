@@ -219,3 +219,28 @@ def test_full_size_properties(rtx_mod, orc, dev_scenes, scene, preset):
     ref, _, _ = oracle_render(orc, scene_path(scene), preset, W, 2, 20, 11, 0, tile=tile)
     rms = np.sqrt(np.mean((crop - ref.reshape(-1, 3)) ** 2))
     assert rms <= RMS_TOL, rms
+
+
+# The reference's error statistic is taken over running sums, so its relative error decays
+# like 0.58/sqrt(n): thresholds ~0.1 make ordinary pixels stop inside these budgets.
+@pytest.mark.parametrize("scene,preset,w,depth,mn,mx,thr", [("three", "c1_three", 32, 10, 4, 24, 0.05),
+                                                            ("final", "c2_final", 32, 50, 8, 32, 0.12),
+                                                            ("cornell", "cornell", 24, 10, 16, 48, 0.1)])
+@pytest.mark.parametrize("precision", ["parity", "fast"])
+def test_megakernel_adaptive_sampler_parity(rtx_mod, orc, dev_scenes, scene, preset, w, depth, mn, mx, thr, precision):
+    """MegaKernel + AdaptiveSampler(min, max, threshold) (sampler.h:44-82): per-pixel sample
+    counts equal the oracle's (pinned to the reference harness by render_mega_adaptive_*)."""
+    thr32 = float(np.float32(thr))
+    cfg = orc.camera_preset(preset)
+    ref, ref_spp, _ = orc.Scene(scene_path(scene)).render(cfg, w, mx, depth, 53, adaptive=1, rng="philox",
+                                                           mode="megakernel", mk_min_samples=mn, mk_threshold=thr32,
+                                                           threads=min(16, os.cpu_count() or 1))
+    cam = rtx_mod.camera(rtx_mod.camera_config(preset, width=w))
+    rgb, sp, _ = dev_scenes(scene).render(cam, mx, depth, seed=53, adaptive=True, mode="megakernel",
+                                          precision=precision, min_spp=mn, rel_threshold=thr32)
+    rms = np.sqrt(np.mean((rgb - ref.reshape(-1, 3)) ** 2))
+    assert rms <= RMS_TOL, rms
+    agree = (sp == ref_spp.ravel()).mean()
+    assert agree >= (1.0 if precision == "parity" else 0.99), agree
+    assert sp.min() >= min(mn, mx + 1) and sp.max() <= mx + 1
+    assert 0 < (sp < mx + 1).mean()  # some pixels converge early
