@@ -291,6 +291,98 @@ int build_fast4(const rtx_bvh_node* n, const rtx_prim* prims, std::vector<F4Node
   return ok ? need : -1;
 }
 
+// Fast-path tree of our own (RTX_FAST_TREE = 1): binned SAH on all three axes (32 bins)
+// over the conservative primitive boxes (prim_box), split down to one primitive per leaf;
+// the result uses the reference node layout (pre-order, leaf = one primitive by its index
+// in the scene's prim array) so build_fast4 collapses it like the reference tree.  The
+// fast path only needs the closest hit among the same primitives, which any conservative
+// tree over them yields (up to exact ties), so the tree itself is free to differ.
+struct SahItem {
+  double lo[3], hi[3], c[3];
+  uint32_t prim;
+};
+static double half_area(const double lo[3], const double hi[3]) {
+  const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+  return dx * dy + dy * dz + dz * dx;
+}
+static int own_sah_node(std::vector<SahItem>& it, int b, int e, std::vector<rtx_bvh_node>& out) {
+  const int me = (int)out.size();
+  out.push_back(rtx_bvh_node{});
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  double clo[3] = {INFINITY, INFINITY, INFINITY}, chi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int i = b; i < e; i++)
+    for (int a = 0; a < 3; a++) {
+      lo[a] = std::min(lo[a], it[i].lo[a]), hi[a] = std::max(hi[a], it[i].hi[a]);
+      clo[a] = std::min(clo[a], it[i].c[a]), chi[a] = std::max(chi[a], it[i].c[a]);
+    }
+  for (int a = 0; a < 3; a++) out[me].lo[a] = lo[a], out[me].hi[a] = hi[a];
+  if (e - b == 1) {
+    out[me].is_leaf = 1, out[me].left_first = it[b].prim, out[me].right_count = 1;
+    return me;
+  }
+  constexpr int kB = 32;
+  int best_axis = -1, best_plane = -1;
+  double best = INFINITY;
+  for (int a = 0; a < 3; a++) {
+    const double ext = chi[a] - clo[a];
+    if (!(ext > 0)) continue;
+    int cnt[kB] = {0};
+    double blo[kB][3], bhi[kB][3];
+    for (int k = 0; k < kB; k++)
+      for (int q = 0; q < 3; q++) blo[k][q] = INFINITY, bhi[k][q] = -INFINITY;
+    const double sc = kB / ext;
+    for (int i = b; i < e; i++) {
+      const int k = std::min(kB - 1, std::max(0, (int)((it[i].c[a] - clo[a]) * sc)));
+      cnt[k]++;
+      for (int q = 0; q < 3; q++) blo[k][q] = std::min(blo[k][q], it[i].lo[q]), bhi[k][q] = std::max(bhi[k][q], it[i].hi[q]);
+    }
+    double rarea[kB];
+    int rcnt[kB];
+    double alo[3] = {INFINITY, INFINITY, INFINITY}, ahi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    int n = 0;
+    for (int k = kB - 1; k >= 1; k--) {
+      n += cnt[k];
+      for (int q = 0; q < 3; q++) alo[q] = std::min(alo[q], blo[k][q]), ahi[q] = std::max(ahi[q], bhi[k][q]);
+      rcnt[k] = n, rarea[k] = n ? half_area(alo, ahi) : 0.0;
+    }
+    for (int q = 0; q < 3; q++) alo[q] = INFINITY, ahi[q] = -INFINITY;
+    n = 0;
+    for (int k = 0; k < kB - 1; k++) {
+      n += cnt[k];
+      for (int q = 0; q < 3; q++) alo[q] = std::min(alo[q], blo[k][q]), ahi[q] = std::max(ahi[q], bhi[k][q]);
+      if (n == 0 || rcnt[k + 1] == 0) continue;
+      const double cost = half_area(alo, ahi) * n + rarea[k + 1] * rcnt[k + 1];
+      if (cost < best) best = cost, best_axis = a, best_plane = k;
+    }
+  }
+  int mid;
+  if (best_axis >= 0) {
+    const double ext = chi[best_axis] - clo[best_axis], sc = kB / ext, c0 = clo[best_axis];
+    auto m = std::partition(it.begin() + b, it.begin() + e, [&](const SahItem& x) {
+      return std::min(kB - 1, std::max(0, (int)((x.c[best_axis] - c0) * sc))) <= best_plane;
+    });
+    mid = (int)(m - it.begin());
+  } else {
+    mid = (b + e) / 2;  // coincident centroids: split the list
+  }
+  if (mid == b || mid == e) mid = (b + e) / 2;
+  const int l = own_sah_node(it, b, mid, out);
+  const int r = own_sah_node(it, mid, e, out);
+  out[me].is_leaf = 0, out[me].left_first = (uint32_t)l, out[me].right_count = (uint32_t)r;
+  return me;
+}
+static void build_own_sah(const rtx_prim* prims, int64_t n, std::vector<rtx_bvh_node>& out) {
+  std::vector<SahItem> it((size_t)n);
+  for (int64_t i = 0; i < n; i++) {
+    prim_box(prims[i], it[i].lo, it[i].hi);
+    for (int a = 0; a < 3; a++) it[i].c[a] = 0.5 * (it[i].lo[a] + it[i].hi[a]);
+    it[i].prim = (uint32_t)i;
+  }
+  out.clear();
+  out.reserve(2 * (size_t)n);
+  if (n > 0) own_sah_node(it, 0, (int)n, out);
+}
+
 int pick_stack(int depth) {
   if (depth + 2 <= 32) return 32;
   if (depth + 2 <= 64) return 64;
@@ -495,7 +587,13 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
     if (sc->stack_parity < 0) return fail(RTX_ERR_INVALID, "BVH deeper than 62 levels");
     if (!d->nodes[0].is_leaf) {
 #if RTX_BVH4
+#if RTX_FAST_TREE
+      std::vector<rtx_bvh_node> own;
+      build_own_sah(d->prims, d->n_prims, own);
+      const int need = build_fast4(own.data(), d->prims, f4);
+#else
       const int need = build_fast4(d->nodes, d->prims, f4);
+#endif
       sc->stack_fast = need < 0 ? -1 : (need <= 32 ? 32 : (need <= 64 ? 64 : -1));
       if (sc->stack_fast > 0 && (rc = upload(sc->fnodes, f4.data(), f4.size(), s))) return rc;
 #else

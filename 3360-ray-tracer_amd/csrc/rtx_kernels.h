@@ -27,6 +27,9 @@ constexpr int kBlock = 256;
 #ifndef RTX_LEAF_SPLIT
 #define RTX_LEAF_SPLIT 2  // BVH4 (A/B r01: 2 = +15% C2, +24% bunny): 0 keep the reference's leaves, 1 open them into one-primitive slots, 2 also as child nodes
 #endif
+#ifndef RTX_FAST_TREE
+#define RTX_FAST_TREE 1  // A/B r01: +2% C2/bunny, +6% C5.  BVH4 source: 0 the reference's SAH tree, 1 our 3-axis SAH tree with 1-prim leaves
+#endif
 #ifndef RTX_BVH4
 #define RTX_BVH4 1  // fast precision traverses the 4-wide collapse of the SAH tree (else BVH2)
 #endif
