@@ -862,7 +862,10 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
     if (mk_adaptive)
       hipLaunchKernelGGL(k_accumulate_mk_adaptive, dim3(pix_blocks), dim3(kBlock), 0, s, px, A.L, npix, Kc,
                          prm->min_spp, prm->spp, prm->rel_threshold);
-    else if (prm->mode == RTX_MODE_MEGAKERNEL)
+    else if (prm->mode == RTX_MODE_MEGAKERNEL || !prm->adaptive)
+      // fixed spp: only sum/(float)samples reaches the output, and the in-order sum is the
+      // same as RecordSample's; the Welford mean/M2 (three divisions per sample) only feed
+      // IsConverged, which adaptive sampling alone consults
       hipLaunchKernelGGL(k_accumulate_sum, dim3(pix_blocks), dim3(kBlock), 0, s, px, A.L, npix, Kc);
     else
       hipLaunchKernelGGL(k_accumulate, dim3(pix_blocks), dim3(kBlock), 0, s, px, A.L, npix, Kc, prm->adaptive,

@@ -12,6 +12,9 @@
 
 #include "rtx.h"
 
+#ifndef RTX_SIGNED_PLANES
+#define RTX_SIGNED_PLANES 1  // A/B r01: +3% C2, -0.7% bunny.  BVH4 slab test with per-ray entry/exit plane selection (no min/max)
+#endif
 #ifndef RTX_PHILOX_MAD
 #define RTX_PHILOX_MAD 1  // A/B r01: +2.3% C2, neutral bunny
 #endif
@@ -183,7 +186,7 @@ static_assert(sizeof(FNode) == 64, "FNode must be one 64-byte line");
 // child < 0: leaf, ~child = first prim, count in 16-bit half (c & 1) of counts[c >> 1];
 // empty slot: an empty leaf (child -1, count 0).  128 bytes = two cache lines.
 struct F4Node {
-  float lox[4], loy[4], loz[4], hix[4], hiy[4], hiz[4];
+  float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4];  // axis a: lo at 32a, hi at 32a + 16 bytes
   int32_t child[4];
   uint32_t counts[2];
   uint32_t pad_[2];
@@ -388,6 +391,45 @@ __device__ __forceinline__ void finish_hit(const DScene& S, int64_t best, V3 o, 
   h.lazy_sphere = (!UV && S.prims[best].kind == RTX_PRIM_SPHERE) ? best : -1;
 }
 
+// The same record from the winner's distance t as traversal computed it (prim_t returns
+// exactly the t that hit_sphere / hit_triangle / hit_rect store), without intersecting again:
+// the remaining fields depend on t and the primitive only.
+template <bool UV = true>
+__device__ __forceinline__ void finish_hit_at(const DScene& S, int64_t best, double t, V3 o, V3 d, Hit& h) {
+  const rtx_prim* __restrict__ P = S.prims + best;
+  const int kind = P->kind;
+  h.u = 0.0, h.v = 0.0;
+  h.mat = P->material;
+  h.t = t;
+  h.lazy_sphere = -1;
+  if (kind == RTX_PRIM_SPHERE) {  // hit_sphere after the root
+    const V3 c{P->g[0], P->g[1], P->g[2]};
+    const double radius = fmax(0.0, P->g[3]);
+    h.p = o + h.t * d;
+    const V3 outward = (h.p - c) / radius;
+    set_face_normal(h, d, outward);
+    if (UV) sphere_uv(outward, h.u, h.v);
+    else h.lazy_sphere = best;
+  } else if (kind == RTX_PRIM_TRIANGLE) {  // hit_triangle after t
+    const V3 A{P->g[0], P->g[1], P->g[2]}, B{P->g[3], P->g[4], P->g[5]}, C{P->g[6], P->g[7], P->g[8]};
+    const V3 e1 = B - A, e2 = C - A;
+    h.p = o + h.t * d;
+    set_face_normal(h, d, normalize(cross(e1, e2)));
+  } else {  // hit_rect after t
+    int a0, a1;
+    V3 n;
+    if (kind == RTX_PRIM_XY_RECT) a0 = 0, a1 = 1, n = v3(0, 0, 1);
+    else if (kind == RTX_PRIM_XZ_RECT) a0 = 0, a1 = 2, n = v3(0, 1, 0);
+    else a0 = 1, a1 = 2, n = v3(1, 0, 0);
+    const double x = comp(o, a0) + t * comp(d, a0);
+    const double y = comp(o, a1) + t * comp(d, a1);
+    h.u = (x - P->g[0]) / (P->g[1] - P->g[0]);
+    h.v = (y - P->g[2]) / (P->g[3] - P->g[2]);
+    set_face_normal(h, d, n);
+    h.p = o + h.t * d;
+  }
+}
+
 // Aabb::Hit (aabb.h:92-115), f64, relies on IEEE 1/0 = inf and false NaN compares.
 __device__ __forceinline__ bool box_hit(const double* lo, const double* hi, V3 o, V3 inv_unused, V3 d,
                                         double tmin, double tmax) {
@@ -433,7 +475,7 @@ __device__ __forceinline__ bool first_active_lane() {
 // Returns the index (leaf order) of the closest primitive, or -1.
 template <int STACK, bool COUNT>
 __device__ __forceinline__ int64_t trace_parity(const DScene& S, V3 o, V3 d, double tmin, double tmax,
-                                                uint32_t* stk, int stride, Counters& cnt) {
+                                                uint32_t* stk, int stride, Counters& cnt, double& t_best) {
   int64_t best = -1;
   double closest = tmax, t;
   if (!S.use_bvh) {  // scene::Scene::Hit linear list (scene.h:47-61)
@@ -441,6 +483,7 @@ __device__ __forceinline__ int64_t trace_parity(const DScene& S, V3 o, V3 d, dou
       if (COUNT) count_prim(cnt, S.prims + i);
       if (prim_t(S.prims + i, o, d, tmin, closest, t)) closest = t, best = i;
     }
+    t_best = closest;
     return best;
   }
   int sp = 0;
@@ -465,6 +508,7 @@ __device__ __forceinline__ int64_t trace_parity(const DScene& S, V3 o, V3 d, dou
       stk[(sp++) * stride] = a;
     }
   }
+  t_best = closest;
   return best;
 }
 
@@ -512,7 +556,7 @@ __device__ __forceinline__ float f32_round_up(double x) {
 
 template <int STACK, bool COUNT>
 __device__ __forceinline__ int64_t trace_fast(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
-                                              int stride, Counters& cnt) {
+                                              int stride, Counters& cnt, double& t_best) {
   int64_t best = -1;
   double closest = tmax, t;
   if (!S.use_bvh || S.froot_leaf) {
@@ -521,6 +565,7 @@ __device__ __forceinline__ int64_t trace_fast(const DScene& S, V3 o, V3 d, doubl
       if (COUNT) count_prim(cnt, S.prims + i);
       if (prim_t(S.prims + i, o, d, tmin, closest, t)) closest = t, best = i;
     }
+    t_best = closest;
     return best;
   }
   const FRay r = make_fray(o, d);
@@ -574,6 +619,7 @@ __device__ __forceinline__ int64_t trace_fast(const DScene& S, V3 o, V3 d, doubl
       node = (int32_t)stk[(--sp) * stride];
     }
   }
+  t_best = closest;
   return best;
 }
 
@@ -597,6 +643,9 @@ __device__ __forceinline__ int64_t trace_fast(const DScene& S, V3 o, V3 d, doubl
 // i.e. the slab imposes no constraint — a widening, hence still conservative.
 struct FRay4 {
   float ix, iy, iz, nlx, nhx, nly, nhy, nlz, nhz;
+#if RTX_SIGNED_PLANES
+  uint32_t ox, oy, oz;  // byte offset of the entry-plane array per axis (exit plane: offset ^ 16)
+#endif
 };
 __device__ __forceinline__ void fray4_axis(double o, double d, float& inv, float& nl, float& nh) {
   inv = 1.0f / (float)d;
@@ -610,12 +659,46 @@ __device__ __forceinline__ void fray4_axis(double o, double d, float& inv, float
   nl = inv >= 0.0f ? n0 - delta : n0 + delta;
   nh = inv >= 0.0f ? n0 + delta : n0 - delta;
 }
+#if RTX_SIGNED_PLANES
+// Sign-selected planes: the entry plane of axis a is `lo` when inv >= 0 and `hi` otherwise,
+// so each slab needs no min/max: nl is the entry offset (n0 - delta), nh the exit offset
+// (n0 + delta), and the entry-plane array is picked by a per-ray byte offset into the node.
+__device__ __forceinline__ void fray4_axis_signed(double o, double d, int axis, float& inv, float& nl, float& nh,
+                                                  uint32_t& off) {
+  inv = 1.0f / (float)d;
+  const float n0 = -((float)o * inv);
+  off = 32u * axis;
+  if (!(fabsf(n0) < __builtin_inff())) {
+    inv = 0.0f, nl = -__builtin_inff(), nh = __builtin_inff();
+    return;
+  }
+  const float delta = fabsf(n0) * 0x1p-20f;
+  nl = n0 - delta, nh = n0 + delta;
+  if (inv < 0.0f) off += 16u;
+}
+#endif
 __device__ __forceinline__ FRay4 make_fray4(V3 o, V3 d) {
   FRay4 r;
+#if RTX_SIGNED_PLANES
+  fray4_axis_signed(o.x, d.x, 0, r.ix, r.nlx, r.nhx, r.ox);
+  fray4_axis_signed(o.y, d.y, 1, r.iy, r.nly, r.nhy, r.oy);
+  fray4_axis_signed(o.z, d.z, 2, r.iz, r.nlz, r.nhz, r.oz);
+#else
   fray4_axis(o.x, d.x, r.ix, r.nlx, r.nhx);
   fray4_axis(o.y, d.y, r.iy, r.nly, r.nhy);
   fray4_axis(o.z, d.z, r.iz, r.nlz, r.nhz);
+#endif
   return r;
+}
+__device__ __forceinline__ float f4c(const float4& v, int c) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); }
+// slab test from entry/exit plane values (sign-selected): entry distance or +inf
+__device__ __forceinline__ float fbox4s(float ex, float ey, float ez, float fx, float fy, float fz, const FRay4& r,
+                                        float tmax_f) {
+  float tn = fmaxf(fmaxf(fmaf(ex, r.ix, r.nlx), fmaf(ey, r.iy, r.nly)), fmaxf(fmaf(ez, r.iz, r.nlz), 0.0f));
+  float tf = fminf(fminf(fmaf(fx, r.ix, r.nhx), fmaf(fy, r.iy, r.nhy)), fminf(fmaf(fz, r.iz, r.nhz), tmax_f));
+  tn = tn * 0.99999f;
+  tf = tf * 1.00001f;
+  return tn <= tf ? tn : __builtin_inff();
 }
 // entry distance (slack-widened) or +inf on a miss; NaN plane distances drop out of the
 // min/max (v_min/v_max_f32 return the non-NaN operand), which only widens the interval
@@ -643,7 +726,7 @@ __device__ __forceinline__ void cswap4(float& ta, int32_t& ca, float& tb, int32_
 
 template <int STACK, bool COUNT>
 __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
-                                               int stride, Counters& cnt) {
+                                               int stride, Counters& cnt, double& t_best) {
   int64_t best = -1;
   double closest = tmax, t;
   if (!S.use_bvh || S.froot_leaf) {
@@ -652,6 +735,7 @@ __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, doub
       if (COUNT) count_prim(cnt, S.prims + i);
       if (prim_t(S.prims + i, o, d, tmin, closest, t)) closest = t, best = i;
     }
+    t_best = closest;
     return best;
   }
   const FRay4 r = make_fray4(o, d);
@@ -667,11 +751,25 @@ __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, doub
     float tt[4];
     int32_t cc[4];
     const uint32_t counts01 = nd->counts[0], counts23 = nd->counts[1];
+#if RTX_SIGNED_PLANES
+    {
+      const char* nb = (const char*)nd;
+      const float4 ex = *(const float4*)(nb + r.ox), fx = *(const float4*)(nb + (r.ox ^ 16u));
+      const float4 ey = *(const float4*)(nb + r.oy), fy = *(const float4*)(nb + (r.oy ^ 16u));
+      const float4 ez = *(const float4*)(nb + r.oz), fz = *(const float4*)(nb + (r.oz ^ 16u));
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        tt[c] = fbox4s(f4c(ex, c), f4c(ey, c), f4c(ez, c), f4c(fx, c), f4c(fy, c), f4c(fz, c), r, tmax_f);
+        cc[c] = nd->child[c];
+      }
+    }
+#else
 #pragma unroll
     for (int c = 0; c < 4; c++) {
       tt[c] = fbox4(nd->lox[c], nd->loy[c], nd->loz[c], nd->hix[c], nd->hiy[c], nd->hiz[c], r, tmax_f);
       cc[c] = nd->child[c];
     }
+#endif
     // hit leaves (non-empty) -> mask; they leave the internal-child ordering
     uint32_t lmask = 0;
 #pragma unroll
@@ -726,6 +824,7 @@ __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, doub
       node = (int32_t)stk[(--sp) * stride];
     }
   }
+  t_best = closest;
   return best;
 }
 

@@ -96,15 +96,16 @@ __device__ __forceinline__ int64_t wave_compact(bool want, unsigned int* counter
   return want ? (int64_t)base + rank : -1;
 }
 
+// Closest primitive (leaf order) or -1; its distance in t_best.
 template <int STACK, bool FAST, bool COUNT>
 __device__ __forceinline__ int64_t trace(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
-                                         Counters& c) {
+                                         Counters& c, double& t_best) {
 #if RTX_BVH4
-  if (FAST) return trace_fast4<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c);
+  if (FAST) return trace_fast4<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best);
 #else
-  if (FAST) return trace_fast<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c);
+  if (FAST) return trace_fast<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best);
 #endif
-  return trace_parity<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c);
+  return trace_parity<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best);
 }
 
 __device__ __forceinline__ void flush_counters(const RenderArgs& A, const Counters& c, uint32_t segs,
@@ -135,12 +136,13 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_intersect(DScene S,
   const rtx_ray r = rays[i];
   V3 o{r.origin[0], r.origin[1], r.origin[2]}, d{r.direction[0], r.direction[1], r.direction[2]};
   Counters c{0, 0, 0, 0, 0, 0};
-  const int64_t best = trace<STACK, FAST, false>(S, o, d, tmin, tmax, stk, c);
+  double tb;
+  const int64_t best = trace<STACK, FAST, false>(S, o, d, tmin, tmax, stk, c, tb);
   rtx_hit out;
   out.pad_ = 0;
   if (best >= 0) {
     Hit h;
-    finish_hit(S, best, o, d, tmin, h);
+    finish_hit_at(S, best, tb, o, d, h);
     out.hit = 1;
     out.front_face = h.front_face, out.material = h.mat, out.t = h.t;
     out.p[0] = h.p.x, out.p[1] = h.p.y, out.p[2] = h.p.z;
@@ -199,7 +201,8 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_wf_extend(RenderArg
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
     const V3 o = v3(q.ox[i], q.oy[i], q.oz[i]);
     const V3 d = v3(q.dx[i], q.dy[i], q.dz[i]);
-    q.hit[i] = (int32_t)trace<STACK, FAST, COUNT>(A.S, o, d, (double)0.001f, kInf, stk, c);
+    double tb;
+    q.hit[i] = (int32_t)trace<STACK, FAST, COUNT>(A.S, o, d, (double)0.001f, kInf, stk, c, tb);
     segs++;
   }
   flush_counters(A, c, segs, 0, COUNT);
@@ -329,10 +332,11 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
       L = v3(0, 0, 0);
       cont = false;
     } else {
-      const int64_t best = trace<STACK, FAST, COUNT>(A.S, P.o, P.d, tmin, kInf, stk, c);
+      double tb;
+      const int64_t best = trace<STACK, FAST, COUNT>(A.S, P.o, P.d, tmin, kInf, stk, c, tb);
       segs++;
       Hit h;
-      if (best >= 0) finish_hit<false>(A.S, best, P.o, P.d, tmin, h);
+      if (best >= 0) finish_hit_at<false>(A.S, best, tb, P.o, P.d, h);
       // stream of this segment: depth + 1 (GetPixel: depth counts down from max_depth)
       Rng g = make_rng(A.seed, pix, smp, SCATTER ? (uint32_t)(A.max_depth - P.depth) + 1u : (uint32_t)P.depth + 1u);
       if (SCATTER) {
