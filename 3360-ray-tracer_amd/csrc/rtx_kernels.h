@@ -272,9 +272,8 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
   bool has = false;
   Path P;
   P.depth = 0;
-  uint64_t slot = 0;
+  uint32_t slot = 0;           // < nslots <= 2^32 - 1 (host check)
   uint32_t pix = 0, smp = 0;  // RNG identity of the lane's path: global pixel, sample
-  const unsigned long long lt = (1ull << lane_id()) - 1ull;
   while (true) {
     // ---- refill: ballot of idle lanes, leftover of the current chunk first.  Refilling
     // only once RTX_REFILL_MIN lanes are idle (or the wave is empty) amortises the
@@ -283,17 +282,18 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
     bool fresh = false;
     if (idle != 0 && !exhausted && (__popcll(idle) >= RTX_REFILL_MIN || idle == ~0ull)) {
       const uint64_t nidle = (uint64_t)__popcll(idle);
-      const uint64_t rank = (uint64_t)__popcll(idle & lt);
+      const uint64_t rank = (uint64_t)__popcll(idle & ((1ull << lane_id()) - 1ull));
+      uint64_t cand = ~0ull;
       if (chunk_left >= nidle) {
-        if (!has) slot = chunk_base + rank, fresh = true;
+        if (!has) cand = chunk_base + rank;
         chunk_base += nidle, chunk_left -= nidle;
       } else {
         unsigned long long nb = 0;
         if (lane_id() == 0) nb = atomicAdd(next_slot, (unsigned long long)kChunk);
         nb = __shfl(nb, 0);
         if (!has) {
-          if (rank < chunk_left) slot = chunk_base + rank, fresh = true;
-          else if (nb < nslots) slot = nb + (rank - chunk_left), fresh = true;
+          if (rank < chunk_left) cand = chunk_base + rank;
+          else if (nb < nslots) cand = nb + (rank - chunk_left);
         }
         if (nb < nslots) {
           const uint64_t used = nidle - chunk_left;
@@ -302,9 +302,10 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
           chunk_left = 0, exhausted = true;
         }
       }
+      if (cand < nslots) slot = (uint32_t)cand, fresh = true;
     }
     // ---- start the primary path of a freshly assigned slot ----
-    if (fresh && slot < nslots) {
+    if (fresh) {
       // nslots < 2^32 (checked on the host): 32-bit division
       const uint32_t p = (uint32_t)slot / (uint32_t)A.K;
       if (!(A.conv && A.conv[p])) {
@@ -364,7 +365,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
       }
     }
     if (!cont) {
-      double* Lp = A.L + 3 * (int64_t)slot;
+      double* Lp = A.L + 3 * (uint64_t)slot;
       Lp[0] = L.x, Lp[1] = L.y, Lp[2] = L.z;
       has = false;
     }

@@ -61,7 +61,9 @@ rtx_render_params DefaultParams(int spp, int max_depth) {
   p.min_spp = 16;                        // wavefront.cc:43
   p.rel_threshold = (double)0.05f;       // wavefront.cc:42 (const float)
   p.seed = 1234;
-  p.mode = RTX_MODE_WAVEFRONT;
+  // the persistent schedule gives the same pixels as the bounce-synchronous wavefront one
+  // (same per-path RNG streams, same per-pixel accumulation order) and is the fast kernel
+  p.mode = RTX_MODE_PERSISTENT;
   p.precision = RTX_PREC_PARITY;
   return p;
 }

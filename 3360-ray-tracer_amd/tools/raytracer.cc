@@ -21,7 +21,7 @@ using namespace rt;
 
 int main(int argc, char** argv) {
   core::Timer clock;
-  std::string preset = "default", scene_name = "cornell", cameras = "cameras.json", mode = "wavefront",
+  std::string preset = "default", scene_name = "cornell", cameras = "cameras.json", mode = "persistent",
               precision = "parity";
   int spp = -1, depth = -1;
   uint64_t seed = 1234;

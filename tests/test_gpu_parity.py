@@ -244,3 +244,19 @@ def test_megakernel_adaptive_sampler_parity(rtx_mod, orc, dev_scenes, scene, pre
     assert agree >= (1.0 if precision == "parity" else 0.99), agree
     assert sp.min() >= min(mn, mx + 1) and sp.max() <= mx + 1
     assert 0 < (sp < mx + 1).mean()  # some pixels converge early
+
+
+@pytest.mark.parametrize("scene,preset,w,spp,depth,adaptive", [("final", "c2_final", 48, 6, 50, 1),
+                                                               ("bunny", "c3_bunny", 40, 4, 20, 0),
+                                                               ("cornell", "cornell", 30, 8, 20, 1)])
+@pytest.mark.parametrize("precision", ["parity", "fast"])
+def test_persistent_schedule_equals_wavefront(rtx_mod, dev_scenes, scene, preset, w, spp, depth, adaptive,
+                                              precision):
+    """The persistent kernel (the default) and the bounce-synchronous wavefront give
+    bit-identical pixels and sample counts: same per-path streams, same accumulation order."""
+    cam = rtx_mod.camera(rtx_mod.camera_config(preset, width=w))
+    a, sa, _ = dev_scenes(scene).render(cam, spp, depth, seed=8, adaptive=adaptive, mode="wavefront",
+                                        precision=precision)
+    b, sb, _ = dev_scenes(scene).render(cam, spp, depth, seed=8, adaptive=adaptive, mode="persistent",
+                                        precision=precision)
+    assert np.array_equal(a, b) and np.array_equal(sa, sb)
