@@ -741,7 +741,10 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
   // samples in flight per pixel (group size K)
   int K = prm->samples_per_group;
   if (K <= 0) {
-    const int64_t target = 1ll << 25;
+    // slots in flight: each persistent launch ends in a tail of draining lanes, so fewer,
+    // larger groups pay it less often (Lbuf = 24 B per slot); the wavefront's two queues cost
+    // 84 B per slot each and keep the smaller target
+    const int64_t target = prm->mode == RTX_MODE_WAVEFRONT ? (1ll << 25) : (1ll << RTX_SLOT_TARGET_LOG2);
     K = (int)std::max<int64_t>(1, std::min<int64_t>(budget > 0 ? budget : 1, target / std::max<int64_t>(1, npix)));
   }
   K = std::max(1, std::min(K, std::max(1, budget)));
@@ -866,7 +869,8 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
       // fixed spp: only sum/(float)samples reaches the output, and the in-order sum is the
       // same as RecordSample's; the Welford mean/M2 (three divisions per sample) only feed
       // IsConverged, which adaptive sampling alone consults
-      hipLaunchKernelGGL(k_accumulate_sum, dim3(pix_blocks), dim3(kBlock), 0, s, px, A.L, npix, Kc);
+      hipLaunchKernelGGL(k_accumulate_sum, dim3((unsigned)((npix + kAccWave - 1) / kAccWave)), dim3(kAccWave), 0, s, px,
+                         A.L, npix, Kc);
     else
       hipLaunchKernelGGL(k_accumulate, dim3(pix_blocks), dim3(kBlock), 0, s, px, A.L, npix, Kc, prm->adaptive,
                          prm->min_spp, prm->rel_threshold);

@@ -33,6 +33,9 @@ constexpr int kBlock = 256;
 #ifndef RTX_BVH4
 #define RTX_BVH4 1  // fast precision traverses the 4-wide collapse of the SAH tree (else BVH2)
 #endif
+#ifndef RTX_SLOT_TARGET_LOG2
+#define RTX_SLOT_TARGET_LOG2 27  // persistent: up to 2^this slots (pixel x sample) per launch (A/B r01: 27 vs 25 = +4% C2, +10% bunny)
+#endif
 #ifndef RTX_REFILL_MIN
 #define RTX_REFILL_MIN 32  // persistent lanes: refill once this many lanes of a wave are idle (A/B: 1/8/16/32)
 #endif
@@ -79,6 +82,15 @@ struct RenderArgs {
   double* L;            // Lbuf: 3 doubles per slot
   unsigned long long* counters;  // [0] segments [1] primaries [2] node visits [3] prim tests
 };
+
+// Per-sample radiance of group slot (pixel p, group sample k) = slot p*K+k, channel c.
+// Pixel-major: the path-end writes of neighbouring lanes (same pixel, consecutive samples)
+// are contiguous.  (Sample-major [k][c][p] coalesces the accumulate's reads but scatters
+// these writes: A/B r01 -2 % C2 and bunny.)
+__device__ __forceinline__ void store_radiance(const RenderArgs& A, uint32_t slot, V3 L) {
+  double* Lp = A.L + 3 * (uint64_t)slot;
+  Lp[0] = L.x, Lp[1] = L.y, Lp[2] = L.z;
+}
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
@@ -235,8 +247,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in,
       V3 L;
       cont = shade(A.S, A.max_depth, P, h, best >= 0, g, L);
       if (!cont) {
-        double* Lp = A.L + 3 * (int64_t)slot;
-        Lp[0] = L.x, Lp[1] = L.y, Lp[2] = L.z;
+        store_radiance(A, (uint32_t)slot, L);
       }
     }
     const int64_t dst = wave_compact(cont, out_count);
@@ -365,8 +376,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
       }
     }
     if (!cont) {
-      double* Lp = A.L + 3 * (uint64_t)slot;
-      Lp[0] = L.x, Lp[1] = L.y, Lp[2] = L.z;
+      store_radiance(A, slot, L);
       has = false;
     }
   }
@@ -421,18 +431,37 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(PixelSoA px, const double
 }
 
 // Fixed-spp megakernel accumulation: DefaultSampler sums GetPixel results in sample order.
-__global__ __launch_bounds__(kBlock) void k_accumulate_sum(PixelSoA px, const double* __restrict__ L, int64_t npix,
-                                                           int K) {
-  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (p >= npix) return;
-  double sum[3];
-  for (int c = 0; c < 3; c++) sum[c] = px.sum[c * npix + p];
-  for (int k = 0; k < K; k++) {
-    const double* x = L + 3 * (p * K + k);
-    for (int c = 0; c < 3; c++) sum[c] += x[c];
+// Fixed-spp sum in sample order (the adds RecordSample does on `sum`).  One wave per 64
+// pixels: chunks of kAccChunk samples are staged through LDS with loads that cover each
+// pixel's contiguous run of 3*kAccChunk doubles, so a load instruction touches a few cache
+// lines instead of 64; each lane then adds its own pixel's samples in order.
+constexpr int kAccWave = 64, kAccChunk = 8, kAccPitch = 3 * kAccChunk + 1;  // odd pitch: 2-way LDS banks
+__global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const double* __restrict__ L, int64_t npix,
+                                                             int K) {
+  __shared__ double st[kAccWave * kAccPitch];
+  const int t = threadIdx.x;
+  const int64_t p0 = (int64_t)blockIdx.x * kAccWave;
+  const int npx = (int)std::min<int64_t>(kAccWave, npix - p0);
+  const int64_t p = p0 + t;
+  double sum[3] = {0, 0, 0};
+  if (t < npx)
+    for (int c = 0; c < 3; c++) sum[c] = px.sum[c * npix + p];
+  for (int k0 = 0; k0 < K; k0 += kAccChunk) {
+    const int kc = std::min(kAccChunk, K - k0), run = 3 * kc, total = npx * run;
+    for (int e = t; e < total; e += kAccWave) {
+      const int q = e / run, j = e - q * run;
+      st[q * kAccPitch + j] = L[(p0 + q) * 3 * (int64_t)K + 3 * k0 + j];
+    }
+    __syncthreads();
+    if (t < npx)
+      for (int k = 0; k < kc; k++)
+        for (int c = 0; c < 3; c++) sum[c] += st[t * kAccPitch + 3 * k + c];
+    __syncthreads();
   }
-  for (int c = 0; c < 3; c++) px.sum[c * npix + p] = sum[c];
-  px.samples[p] += K;
+  if (t < npx) {
+    for (int c = 0; c < 3; c++) px.sum[c * npix + p] = sum[c];
+    px.samples[p] += K;
+  }
 }
 
 // AdaptiveSampler::SamplePixel (sampler.h:44-82) replayed in sample order for the MegaKernel
