@@ -561,7 +561,20 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   hipStream_t s = sc->stream;
   int rc;
   if ((rc = upload(sc->prims, d->prims, d->n_prims, s))) return rc;
-  if ((rc = upload(sc->mats, d->materials, d->n_materials, s))) return rc;
+  // Device copy of the material table: a Lambertian / DiffuseLight whose texture is a
+  // SolidColor carries the colour itself (texture = -1, colour in the unused albedo field),
+  // so shading skips the dependent texture-table load (mat_tex, rtx_device.h).
+  std::vector<rtx_material> dmats(d->materials, d->materials + d->n_materials);
+#if RTX_MAT_SOLID_INLINE
+  for (rtx_material& m : dmats) {
+    if ((m.kind == RTX_MAT_LAMBERTIAN || m.kind == RTX_MAT_DIFFUSE_LIGHT) && m.texture >= 0 &&
+        d->textures[m.texture].kind == RTX_TEX_SOLID) {
+      for (int c = 0; c < 3; c++) m.albedo[c] = d->textures[m.texture].color[c];
+      m.texture = -1;
+    }
+  }
+#endif
+  if ((rc = upload(sc->mats, dmats.data(), d->n_materials, s))) return rc;
   if ((rc = upload(sc->texs, d->textures, d->n_textures, s))) return rc;
   std::vector<DImage> imgs(d->n_images);
   sc->texels.resize(d->n_images);
@@ -615,6 +628,8 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   S.use_bvh = (d->nodes && d->n_nodes > 0) ? 1 : 0;
   S.n_prims = S.use_bvh ? d->n_prims : d->n_prims;
   S.froot_leaf = 0, S.froot_count = 0;
+  S.has_tris = 0;
+  for (int64_t i = 0; i < d->n_prims && !S.has_tris; i++) S.has_tris = d->prims[i].kind == RTX_PRIM_TRIANGLE;
   if (S.use_bvh && d->nodes[0].is_leaf) S.froot_leaf = 1, S.froot_count = (int32_t)d->nodes[0].right_count;
   if (!d->nodes && d->n_nodes == 0) S.use_bvh = 0;
   *out = sc.release();

@@ -18,6 +18,12 @@
 #ifndef RTX_PHILOX_MAD
 #define RTX_PHILOX_MAD 1  // A/B r01: +2.3% C2, neutral bunny
 #endif
+#ifndef RTX_PRIM_PRELOAD
+#define RTX_PRIM_PRELOAD 1  // primitive record in one batch of loads before the kind branch
+#endif
+#ifndef RTX_MAT_SOLID_INLINE
+#define RTX_MAT_SOLID_INLINE 1  // solid-colour textures resolved into the device material table
+#endif
 
 namespace rtxd {
 
@@ -205,7 +211,7 @@ struct DScene {
   int32_t use_bvh;
   int32_t froot_leaf;  // fast BVH: the whole tree is one leaf (count in froot_count)
   int32_t froot_count;
-  int32_t pad_;
+  int32_t has_tris;  // any triangle: prim_t preloads all 80 record bytes, else the first 48
 };
 
 struct Hit {  // HitRecord (hittable.h:18-42)
@@ -330,8 +336,45 @@ __device__ __forceinline__ bool hit_prim(const rtx_prim* __restrict__ P, V3 o, V
 // Traversal keeps just (closest t, best primitive); finish_hit() rebuilds the record of the
 // winner afterwards with the interval (tmin, +inf), which yields the same root/t and hence
 // the identical record (sphere: the near root is re-selected iff it was accepted).
-__device__ __forceinline__ bool prim_t(const rtx_prim* __restrict__ P, V3 o, V3 d, double tmin, double tmax,
-                                       double& t_out) {
+//
+// The 80-byte record is fetched as five 16-byte loads issued together, before the branch on
+// `kind`: one memory latency per primitive test instead of two (kind, then the geometry
+// the kind selects).  The empty asm keeps the compiler from sinking the geometry loads into
+// the branches.
+struct PrimRec {
+  int kind;
+  int32_t mat;
+  double g[9];
+};
+__device__ __forceinline__ PrimRec load_prim(const rtx_prim* __restrict__ P, bool tris) {
+  PrimRec r;
+#if RTX_PRIM_PRELOAD
+  // spheres and rects read g[0..4] (48 bytes); triangles g[0..8] (80 bytes)
+  const uint4 w0 = *(const uint4*)P;
+  const double2 w1 = *((const double2*)P + 1), w2 = *((const double2*)P + 2);
+  double2 w3 = make_double2(0.0, 0.0), w4 = make_double2(0.0, 0.0);
+  if (tris) w3 = *((const double2*)P + 3), w4 = *((const double2*)P + 4);
+  asm volatile("" ::"v"(w0.x), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w2.x), "v"(w2.y), "v"(w3.x),
+               "v"(w3.y), "v"(w4.x), "v"(w4.y));
+  r.kind = (int)w0.x;
+  r.mat = (int32_t)w0.y;
+  r.g[0] = __hiloint2double((int)w0.w, (int)w0.z);
+  r.g[1] = w1.x, r.g[2] = w1.y, r.g[3] = w2.x, r.g[4] = w2.y;
+  r.g[5] = w3.x, r.g[6] = w3.y, r.g[7] = w4.x, r.g[8] = w4.y;
+#else
+  r.kind = P->kind;
+  r.mat = P->material;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r.g[i] = P->g[i];
+#endif
+  return r;
+}
+
+__device__ __forceinline__ bool prim_t(const rtx_prim* __restrict__ Pp, bool tris, V3 o, V3 d, double tmin,
+                                       double tmax, double& t_out, int32_t& mat_out) {
+  const PrimRec R = load_prim(Pp, tris);
+  mat_out = R.mat;
+  const PrimRec* P = &R;
   const int kind = P->kind;
   if (kind == RTX_PRIM_TRIANGLE) {
     V3 A{P->g[0], P->g[1], P->g[2]}, B{P->g[3], P->g[4], P->g[5]}, C{P->g[6], P->g[7], P->g[8]};
@@ -380,6 +423,12 @@ __device__ __forceinline__ bool prim_t(const rtx_prim* __restrict__ P, V3 o, V3 
   if (x < P->g[0] || x > P->g[1] || y < P->g[2] || y > P->g[3]) return false;
   t_out = t;
   return true;
+}
+
+__device__ __forceinline__ bool prim_t(const rtx_prim* __restrict__ P, bool tris, V3 o, V3 d, double tmin,
+                                       double tmax, double& t_out) {
+  int32_t m;
+  return prim_t(P, tris, o, d, tmin, tmax, t_out, m);
 }
 
 // Rebuild the HitRecord of the closest primitive (see prim_t).  u, v start at 0: the
@@ -481,7 +530,7 @@ __device__ __forceinline__ int64_t trace_parity(const DScene& S, V3 o, V3 d, dou
   if (!S.use_bvh) {  // scene::Scene::Hit linear list (scene.h:47-61)
     for (int64_t i = 0; i < S.n_prims; i++) {
       if (COUNT) count_prim(cnt, S.prims + i);
-      if (prim_t(S.prims + i, o, d, tmin, closest, t)) closest = t, best = i;
+      if (prim_t(S.prims + i, S.has_tris, o, d, tmin, closest, t)) closest = t, best = i;
     }
     t_best = closest;
     return best;
@@ -500,7 +549,7 @@ __device__ __forceinline__ int64_t trace_parity(const DScene& S, V3 o, V3 d, dou
     if (leaf) {
       for (uint32_t i = 0; i < b; i++) {
         if (COUNT) count_prim(cnt, S.prims + a + i);
-        if (prim_t(S.prims + a + i, o, d, tmin, closest, t)) closest = t, best = (int64_t)a + i;
+        if (prim_t(S.prims + a + i, S.has_tris, o, d, tmin, closest, t)) closest = t, best = (int64_t)a + i;
       }
     } else {
       if (sp + 2 > STACK) __builtin_trap();  // host sizes STACK >= tree depth + 1
@@ -563,7 +612,7 @@ __device__ __forceinline__ int64_t trace_fast(const DScene& S, V3 o, V3 d, doubl
     const int64_t n = S.use_bvh ? S.froot_count : S.n_prims;
     for (int64_t i = 0; i < n; i++) {
       if (COUNT) count_prim(cnt, S.prims + i);
-      if (prim_t(S.prims + i, o, d, tmin, closest, t)) closest = t, best = i;
+      if (prim_t(S.prims + i, S.has_tris, o, d, tmin, closest, t)) closest = t, best = i;
     }
     t_best = closest;
     return best;
@@ -589,7 +638,7 @@ __device__ __forceinline__ int64_t trace_fast(const DScene& S, V3 o, V3 d, doubl
       uint32_t first = (uint32_t)(~c0);
       for (uint32_t i = 0; i < n0; i++) {
         if (COUNT) count_prim(cnt, S.prims + first + i);
-        if (prim_t(S.prims + first + i, o, d, tmin, closest, t)) closest = t, best = (int64_t)first + i, shrink = true;
+        if (prim_t(S.prims + first + i, S.has_tris, o, d, tmin, closest, t)) closest = t, best = (int64_t)first + i, shrink = true;
       }
       h0 = false;
     }
@@ -597,7 +646,7 @@ __device__ __forceinline__ int64_t trace_fast(const DScene& S, V3 o, V3 d, doubl
       uint32_t first = (uint32_t)(~c1);
       for (uint32_t i = 0; i < n1; i++) {
         if (COUNT) count_prim(cnt, S.prims + first + i);
-        if (prim_t(S.prims + first + i, o, d, tmin, closest, t)) closest = t, best = (int64_t)first + i, shrink = true;
+        if (prim_t(S.prims + first + i, S.has_tris, o, d, tmin, closest, t)) closest = t, best = (int64_t)first + i, shrink = true;
       }
       h1 = false;
     }
@@ -726,14 +775,16 @@ __device__ __forceinline__ void cswap4(float& ta, int32_t& ca, float& tb, int32_
 
 template <int STACK, bool COUNT>
 __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
-                                               int stride, Counters& cnt, double& t_best) {
+                                               int stride, Counters& cnt, double& t_best, int32_t& mat_best) {
   int64_t best = -1;
   double closest = tmax, t;
+  int32_t m;
+  mat_best = -1;
   if (!S.use_bvh || S.froot_leaf) {
     const int64_t n = S.use_bvh ? S.froot_count : S.n_prims;
     for (int64_t i = 0; i < n; i++) {
       if (COUNT) count_prim(cnt, S.prims + i);
-      if (prim_t(S.prims + i, o, d, tmin, closest, t)) closest = t, best = i;
+      if (prim_t(S.prims + i, S.has_tris, o, d, tmin, closest, t, m)) closest = t, best = i, mat_best = m;
     }
     t_best = closest;
     return best;
@@ -787,15 +838,17 @@ __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, doub
         if (left == 0) {
           const int c = __builtin_ctz(lmask);
           lmask &= lmask - 1u;
-          const int32_t ch = c == 0 ? cc[0] : (c == 1 ? cc[1] : (c == 2 ? cc[2] : cc[3]));
-          cur = (uint32_t)(~ch);
-          left = ((c < 2 ? counts01 : counts23) >> (16 * (c & 1))) & 0xffffu;
+          // two-level select (v_cndmask) rather than a compare chain the compiler branches on
+          const int32_t c01 = (c & 1) ? cc[1] : cc[0], c23 = (c & 1) ? cc[3] : cc[2];
+          cur = (uint32_t)(~((c & 2) ? c23 : c01));
+          left = (((c & 2) ? counts23 : counts01) >> (16 * (c & 1))) & 0xffffu;
         }
         if (COUNT) {
           count_prim(cnt, S.prims + cur);
           if (first_active_lane()) cnt.wprims++;
         }
-        if (prim_t(S.prims + cur, o, d, tmin, closest, t)) closest = t, best = (int64_t)cur, shrink = true;
+        if (prim_t(S.prims + cur, S.has_tris, o, d, tmin, closest, t, m))
+          closest = t, best = (int64_t)cur, mat_best = m, shrink = true;
         cur++, left--;
       }
       if (shrink) {
@@ -869,6 +922,15 @@ __device__ __forceinline__ V3 tex_value(const DScene& S, int32_t t, const Hit& r
   return v3(0, 1, 1);
 }
 
+// Albedo / emission texture of a Lambertian or DiffuseLight material.  The device copy of
+// the material table (rtx_scene_create) resolves a directly attached SolidColor texture at
+// upload: texture = -1 and the colour's doubles copied into the (otherwise unused) albedo
+// field, so the common case costs no dependent texture-table load.
+__device__ __forceinline__ V3 mat_tex(const DScene& S, const rtx_material& m, const Hit& rec) {
+  if (m.texture < 0) return v3(m.albedo[0], m.albedo[1], m.albedo[2]);
+  return tex_value(S, m.texture, rec);
+}
+
 // pow(x, 5.0) (material.cc:261) as a double-double product chain rounded once: the
 // correctly rounded x^5, which is what glibc's pow (<= 0.52 ulp) returns except at
 // near-ties.  Explicit fma() only builds the exact error terms (no contraction elsewhere).
@@ -894,7 +956,7 @@ __device__ __forceinline__ bool mat_sample(const DScene& S, const rtx_material& 
     float c = (float)dot(rec.normal, wi);
     pdf = (c <= 0.0f) ? 0.0f : (float)((double)c / kPi);
     if (dot(rec.normal, wi) <= 0) f = v3(0, 0, 0);
-    else f = tex_value(S, m.texture, rec) / kPi;
+    else f = mat_tex(S, m, rec) / kPi;
     return true;
   }
   if (m.kind == RTX_MAT_METAL) {
@@ -946,7 +1008,7 @@ __device__ __forceinline__ bool mat_scatter(const DScene& S, const rtx_material&
     V3 dir = rec.normal + random_unit_vector(g);
     if (near_zero(dir)) dir = rec.normal;
     sd = dir;
-    att = tex_value(S, m.texture, rec);
+    att = mat_tex(S, m, rec);
     return true;
   }
   if (m.kind == RTX_MAT_METAL) {
@@ -971,7 +1033,7 @@ __device__ __forceinline__ bool mat_scatter(const DScene& S, const rtx_material&
 }
 
 __device__ __forceinline__ V3 mat_emitted(const DScene& S, const rtx_material& m, const Hit& rec) {
-  if (m.kind == RTX_MAT_DIFFUSE_LIGHT) return tex_value(S, m.texture, rec);
+  if (m.kind == RTX_MAT_DIFFUSE_LIGHT) return mat_tex(S, m, rec);
   return v3(0, 0, 0);
 }
 
@@ -1010,14 +1072,14 @@ struct Path {
 
 // One shading step (wavefront.cc:109-208).  true: continue with p updated; false: path
 // terminated with radiance L (RecordSample is done by the caller, in sample order).
+// `m` is the hit's material (S.mats[rec.mat]; unused on a miss).
 __device__ __forceinline__ bool shade(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit, Rng& g,
-                                      V3& L) {
+                                      V3& L, const rtx_material& m) {
   L = v3(0, 0, 0);
   if (!hit || p.depth >= max_depth) {
     L = L + p.thr * sky(p.d);
     return false;
   }
-  const rtx_material m = S.mats[rec.mat];
   V3 em = mat_emitted(S, m, rec);
   if (!near_zero(em)) {
     L = L + p.thr * em;
@@ -1044,6 +1106,13 @@ __device__ __forceinline__ bool shade(const DScene& S, int max_depth, Path& p, c
   }
   p = c;
   return true;
+}
+
+__device__ __forceinline__ bool shade(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit, Rng& g,
+                                      V3& L) {
+  rtx_material m;
+  if (hit) m = S.mats[rec.mat];
+  return shade(S, max_depth, p, rec, hit, g, L, m);
 }
 
 }  // namespace rtxd

@@ -36,6 +36,9 @@ constexpr int kBlock = 256;
 #ifndef RTX_SLOT_TARGET_LOG2
 #define RTX_SLOT_TARGET_LOG2 27  // persistent: up to 2^this slots (pixel x sample) per launch (A/B r01: 27 vs 25 = +4% C2, +10% bunny)
 #endif
+#ifndef RTX_EARLY_MAT
+#define RTX_EARLY_MAT 0  // persistent: material fetched by the id the traversal kept, beside the record (A/B r01: -2% C2, +-0 bunny)
+#endif
 #ifndef RTX_REFILL_MIN
 #define RTX_REFILL_MIN 32  // persistent lanes: refill once this many lanes of a wave are idle (A/B: 1/8/16/32)
 #endif
@@ -109,15 +112,27 @@ __device__ __forceinline__ int64_t wave_compact(bool want, unsigned int* counter
 }
 
 // Closest primitive (leaf order) or -1; its distance in t_best.
+// mat_best: the closest primitive's material id (or -1); the fast traversal keeps it from the
+// primitive record it already loaded, so shading can fetch the material without first
+// waiting for the record.
+template <int STACK, bool FAST, bool COUNT>
+__device__ __forceinline__ int64_t trace(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
+                                         Counters& c, double& t_best, int32_t& mat_best) {
+#if RTX_BVH4
+  if (FAST) return trace_fast4<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best, mat_best);
+  const int64_t b = trace_parity<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best);
+#else
+  const int64_t b = FAST ? trace_fast<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best)
+                         : trace_parity<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best);
+#endif
+  mat_best = b >= 0 ? S.prims[b].material : -1;
+  return b;
+}
 template <int STACK, bool FAST, bool COUNT>
 __device__ __forceinline__ int64_t trace(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
                                          Counters& c, double& t_best) {
-#if RTX_BVH4
-  if (FAST) return trace_fast4<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best);
-#else
-  if (FAST) return trace_fast<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best);
-#endif
-  return trace_parity<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best);
+  int32_t m;
+  return trace<STACK, FAST, COUNT>(S, o, d, tmin, tmax, stk, c, t_best, m);
 }
 
 __device__ __forceinline__ void flush_counters(const RenderArgs& A, const Counters& c, uint32_t segs,
@@ -345,10 +360,19 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
       cont = false;
     } else {
       double tb;
-      const int64_t best = trace<STACK, FAST, COUNT>(A.S, P.o, P.d, tmin, kInf, stk, c, tb);
+      int32_t bmat;
+      const int64_t best = trace<STACK, FAST, COUNT>(A.S, P.o, P.d, tmin, kInf, stk, c, tb, bmat);
       segs++;
       Hit h;
+      rtx_material m;
+#if RTX_EARLY_MAT
+      // the material load is in flight together with the winner's record (finish_hit_at)
+      if (best >= 0) m = A.S.mats[bmat];
+#endif
       if (best >= 0) finish_hit_at<false>(A.S, best, tb, P.o, P.d, h);
+#if !RTX_EARLY_MAT
+      if (best >= 0) m = A.S.mats[h.mat];
+#endif
       // stream of this segment: depth + 1 (GetPixel: depth counts down from max_depth)
       Rng g = make_rng(A.seed, pix, smp, SCATTER ? (uint32_t)(A.max_depth - P.depth) + 1u : (uint32_t)P.depth + 1u);
       if (SCATTER) {
@@ -359,7 +383,6 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
           L = P.thr * sky(P.d);
           cont = false;
         } else {
-          const rtx_material m = A.S.mats[h.mat];
           V3 att, sd;
           if (mat_scatter(A.S, m, P.d, h, att, sd, g)) {
             P.thr = P.thr * att;
@@ -372,7 +395,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
           }
         }
       } else {
-        cont = shade(A.S, A.max_depth, P, h, best >= 0, g, L);
+        cont = shade(A.S, A.max_depth, P, h, best >= 0, g, L, m);
       }
     }
     if (!cont) {
