@@ -574,6 +574,17 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
     }
   }
 #endif
+  // Dielectric: eta on a front-face hit (eta_i / eta_t = 1 / ri) and Schlick's r0 for
+  // reflectance(c, ri) (material.cc:226-262) in the unused albedo field, computed with the same
+  // IEEE double operations the kernel would perform (shade_merged, rtx_device.h).
+  for (rtx_material& m : dmats) {
+    if (m.kind != RTX_MAT_DIELECTRIC) continue;
+    const double ri = m.ref_idx;
+    double r0 = (1.0 - ri) / (1.0 + ri);
+    r0 = r0 * r0;
+    m.albedo[0] = 1.0 / ri;
+    m.albedo[1] = r0;
+  }
   if ((rc = upload(sc->mats, dmats.data(), d->n_materials, s))) return rc;
   if ((rc = upload(sc->texs, d->textures, d->n_textures, s))) return rc;
   std::vector<DImage> imgs(d->n_images);
@@ -914,6 +925,13 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
     stats->tri_tests = h[6];
     stats->sphere_tests = h[7];
     stats->node_bytes = (L.fast && RTX_BVH4) ? sizeof(F4Node) : (L.fast ? sizeof(FNode) : sizeof(rtx_bvh_node));
+#if RTX_STAMPS
+    unsigned long long st[4];
+    HIPC(hipMemcpy(st, cnt + 24, sizeof st, hipMemcpyDeviceToHost));
+    const double tot = (double)(st[0] + st[1] + st[2] + st[3]);
+    fprintf(stderr, "rtx stamps (wave cycles): refill %.3f trace %.3f shade %.3f other %.3f total %.4g\n",
+            st[0] / tot, st[1] / tot, st[2] / tot, st[3] / tot, tot);
+#endif
   }
   return RTX_OK;
 }

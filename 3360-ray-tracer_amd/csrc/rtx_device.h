@@ -21,6 +21,9 @@
 #ifndef RTX_PRIM_PRELOAD
 #define RTX_PRIM_PRELOAD 1  // primitive record in one batch of loads before the kind branch
 #endif
+#ifndef RTX_MERGED_SHADE
+#define RTX_MERGED_SHADE 1  // Sample() chains of the three materials in shared normalize/sqrt slots
+#endif
 #ifndef RTX_MAT_SOLID_INLINE
 #define RTX_MAT_SOLID_INLINE 1  // solid-colour textures resolved into the device material table
 #endif
@@ -1070,11 +1073,162 @@ struct Path {
   int32_t depth;
 };
 
+// Pins a value at this point of the program (no code): the shared shading slots below stay
+// single instances instead of being sunk into the per-material branches that use them.
+__device__ __forceinline__ void pin(double& x) { asm volatile("" : "+v"(x)); }
+__device__ __forceinline__ void pin(V3& v) {
+  pin(v.x);
+  pin(v.y);
+  pin(v.z);
+}
+// normalize (math_utils.h:93-97) returning the length as well
+__device__ __forceinline__ V3 normalize_l(V3 v, double& l) {
+  l = sqrt(len2(v));
+  if (l == 0.0) return {0, 0, 0};
+  return v / l;
+}
+
 // One shading step (wavefront.cc:109-208).  true: continue with p updated; false: path
 // terminated with radiance L (RecordSample is done by the caller, in sample order).
 // `m` is the hit's material (S.mats[rec.mat]; unused on a miss).
-__device__ __forceinline__ bool shade(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit, Rng& g,
-                                      V3& L, const rtx_material& m) {
+//
+// The Sample() chains of the three materials (material.cc:57-74, 117-141, 194-256) are run
+// in five shared slots: a wave that holds lanes of several materials executes each
+// normalize / sqrt once for all of them, instead of once per material branch.  Every lane
+// still performs exactly its own material's operations on its own operands, in the
+// reference's order, so the results are bit-identical to shade_by_material below:
+//   slot 1 normalize   Lambertian: w = normalize(n)          Dielectric: win = normalize(d)
+//   slot 2 sqrt        Lambertian: sqrt(r2)                  Dielectric: sqrt(max(0, 1 - ci^2))
+//   slot 3 sqrt        Lambertian: sqrt(1 - r2)              Dielectric (refract): sqrt|1 - |perp|^2|
+//   slot 4 normalize   Lambertian: normalize(cross(w, a))    Metal: normalize(reflect + fuzz * u)
+//   slot 5 normalize   Lambertian: normalize(x u + y v + z w)
+// The ray's unit direction is shared too: sky() on a miss and wo = -normalize(d) on a hit.
+// Dielectric uses win = -normalize(wo) = normalize(normalize(d)) exactly (sign-symmetric
+// rounding), and eta = 1/ri (front face) / r0 = ((1-ri)/(1+ri))^2 precomputed at upload
+// in the same IEEE double operations (device material table, rtx_scene_create).
+__device__ __forceinline__ bool shade_merged(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit,
+                                             Rng& g, V3& L, const rtx_material& m) {
+  L = v3(0, 0, 0);
+  double lnd;
+  const V3 nd = normalize_l(p.d, lnd);  // wo = -nd (hit), sky(d) (miss)
+  if (!hit || p.depth >= max_depth) {
+    const double t = 0.5 * (nd.y + 1.0);  // sky() with ud = nd
+    L = L + p.thr * ((1.0 - t) * v3(1.0, 1.0, 1.0) + t * v3(0.5, 0.7, 1.0));
+    return false;
+  }
+  V3 em = mat_emitted(S, m, rec);
+  if (!near_zero(em)) {
+    L = L + p.thr * em;
+    return false;
+  }
+  const int kind = m.kind;
+  const bool isL = kind == RTX_MAT_LAMBERTIAN, isM = kind == RTX_MAT_METAL, isG = kind == RTX_MAT_DIELECTRIC;
+  if (!(isL || isM || isG)) return false;  // DiffuseLight::Sample
+  const V3 n = rec.normal;
+  double r1 = 0.0, r2 = 0.0;
+  if (isL) r1 = g.next(), r2 = g.next();
+  V3 ru = v3(0, 0, 0);
+  if (isM) ru = random_unit_vector(g);
+  // ---- slot 1: normalize
+  double l1;
+  V3 s1 = normalize_l(isL ? n : nd, l1);
+  pin(s1);
+  const V3 w = s1;
+  // win = -normalize(wo): (0,0,0) negated when the direction has zero length
+  const V3 win = (!isL && l1 == 0.0) ? v3(-0.0, -0.0, -0.0) : s1;
+  double eta = 0.0, ci = 0.0, a2 = 0.0;
+  if (isG) {
+    eta = rec.front_face ? m.albedo[0] : m.ref_idx;  // eta_i / eta_t
+    ci = dot(win, n);
+    ci = ci < -1.0 ? -1.0 : (ci > 1.0 ? 1.0 : ci);
+    a2 = fmax(0.0, 1.0 - ci * ci);
+  }
+  // ---- slot 2: sqrt
+  double s2 = sqrt(isL ? r2 : a2);
+  pin(s2);
+  double x = 0.0, y = 0.0;
+  if (isL) {
+    const double phi = 2.0 * kPi * r1;
+    x = s2 * cos(phi);
+    y = s2 * sin(phi);
+  }
+  bool g_reflect = false;
+  V3 perp = v3(0, 0, 0);
+  double a3 = 1.0;
+  if (isG) {
+    const double st = eta * s2;
+    g_reflect = st >= 1.0;
+    if (!g_reflect) {
+      const double r0 = m.albedo[1];  // reflectance(|ci|, ref_idx): r0 = ((1-ri)/(1+ri))^2
+      const double Fr = r0 + (1.0 - r0) * pow5(1.0 - fabs(ci));
+      g_reflect = g.next() < Fr;
+    }
+    if (!g_reflect) {  // refract (math_utils.h:24-29)
+      const double c = fmin(dot(-win, n), 1.0);
+      perp = eta * (win + c * n);
+      a3 = fabs(1.0 - len2(perp));
+    }
+  }
+  // ---- slot 3: sqrt
+  double s3 = sqrt(isL ? 1.0 - r2 : a3);
+  pin(s3);
+  V3 in4;
+  if (isL) {
+    const V3 a = (fabs(w.x) > 0.9) ? v3(0, 1, 0) : v3(1, 0, 0);
+    in4 = cross(w, a);
+  } else {
+    in4 = reflect(nd, n);  // reflect(-wo, n)
+    in4 = in4 + m.fuzz * ru;
+  }
+  // ---- slot 4: normalize
+  double l4;
+  V3 s4 = normalize_l(in4, l4);
+  pin(s4);
+  V3 wi, f;
+  Path c;
+  c.o = rec.p, c.depth = p.depth + 1;
+  if (isL) {
+    const V3 v = s4;
+    const V3 u = cross(v, w);
+    // ---- slot 5: normalize (Lambertian only)
+    wi = normalize(x * u + y * v + s3 * w);
+    if (dot(wi, n) <= 0) return false;
+    const float cf = (float)dot(n, wi);
+    const float pdf = (cf <= 0.0f) ? 0.0f : (float)((double)cf / kPi);
+    f = mat_tex(S, m, rec) / kPi;
+    if (pdf < 1e-6f) return false;
+    const float ct = fmaxf(0.0f, (float)dot(wi, n));
+    c.thr = ((double)ct * (p.thr * f)) / (double)pdf;
+  } else if (isM) {
+    wi = s4;
+    if (dot(wi, n) <= 0) return false;
+    c.thr = p.thr * v3(m.albedo[0], m.albedo[1], m.albedo[2]);
+  } else {
+    if (g_reflect) {
+      wi = reflect(win, n);
+      c.thr = p.thr * v3(1.0, 1.0, 1.0);
+    } else {
+      const V3 par = (-s3) * n;
+      wi = perp + par;
+      const double k = eta * eta;
+      c.thr = p.thr * v3(k, k, k);
+    }
+  }
+  c.d = wi;
+  if (c.depth > 5) {  // Russian roulette (wavefront.cc:189-205)
+    double q = fmax(fmax(c.thr.x, c.thr.y), c.thr.z);
+    q = q < 0.1 ? 0.1 : (q > 0.95 ? 0.95 : q);
+    if (g.next() > q) return false;
+    c.thr = c.thr / q;
+  }
+  p = c;
+  return true;
+}
+
+// The same step with one Sample() branch per material (mat_sample): the reference's
+// structure, kept for the A/B build (RTX_MERGED_SHADE=0) and as the readable statement.
+__device__ __forceinline__ bool shade_by_material(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit,
+                                                  Rng& g, V3& L, const rtx_material& m) {
   L = v3(0, 0, 0);
   if (!hit || p.depth >= max_depth) {
     L = L + p.thr * sky(p.d);
@@ -1106,6 +1260,16 @@ __device__ __forceinline__ bool shade(const DScene& S, int max_depth, Path& p, c
   }
   p = c;
   return true;
+}
+
+
+__device__ __forceinline__ bool shade(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit, Rng& g,
+                                      V3& L, const rtx_material& m) {
+#if RTX_MERGED_SHADE
+  return shade_merged(S, max_depth, p, rec, hit, g, L, m);
+#else
+  return shade_by_material(S, max_depth, p, rec, hit, g, L, m);
+#endif
 }
 
 __device__ __forceinline__ bool shade(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit, Rng& g,

@@ -36,6 +36,9 @@ constexpr int kBlock = 256;
 #ifndef RTX_SLOT_TARGET_LOG2
 #define RTX_SLOT_TARGET_LOG2 27  // persistent: up to 2^this slots (pixel x sample) per launch (A/B r01: 27 vs 25 = +4% C2, +10% bunny)
 #endif
+#ifndef RTX_STAMPS
+#define RTX_STAMPS 0  // diagnostic build: s_memtime per region of k_persistent -> counters[24..27]
+#endif
 #ifndef RTX_EARLY_MAT
 #define RTX_EARLY_MAT 0  // persistent: material fetched by the id the traversal kept, beside the record (A/B r01: -2% C2, +-0 bunny)
 #endif
@@ -282,7 +285,10 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in,
 // (miss, emitter, absorption, Russian roulette) are immediately given a new primary —
 // the per-wave __ballot of idle lanes is the active-ray compaction.
 // ---------------------------------------------------------------------------------------
-constexpr int kChunk = 256;
+#ifndef RTX_CHUNK
+#define RTX_CHUNK 256  // persistent: slots taken per atomic on the global slot counter
+#endif
+constexpr int kChunk = RTX_CHUNK;
 
 template <int STACK, bool FAST, bool COUNT, bool SCATTER>
 __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderArgs A, unsigned long long* next_slot) {
@@ -300,6 +306,18 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
   P.depth = 0;
   uint32_t slot = 0;           // < nslots <= 2^32 - 1 (host check)
   uint32_t pix = 0, smp = 0;  // RNG identity of the lane's path: global pixel, sample
+#if RTX_STAMPS
+  uint64_t cyc[4] = {0, 0, 0, 0};
+  uint64_t ts = __builtin_amdgcn_s_memtime();
+#define RTX_STAMP(i)                                   \
+  {                                                    \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();  \
+    cyc[i] += t_ - ts;                                 \
+    ts = t_;                                           \
+  }
+#else
+#define RTX_STAMP(i)
+#endif
   while (true) {
     // ---- refill: ballot of idle lanes, leftover of the current chunk first.  Refilling
     // only once RTX_REFILL_MIN lanes are idle (or the wave is empty) amortises the
@@ -347,6 +365,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
         prims++;
       }
     }
+    RTX_STAMP(0)
     if (!__any(has)) {
       if (exhausted) break;
       continue;
@@ -362,6 +381,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
       double tb;
       int32_t bmat;
       const int64_t best = trace<STACK, FAST, COUNT>(A.S, P.o, P.d, tmin, kInf, stk, c, tb, bmat);
+      RTX_STAMP(1)
       segs++;
       Hit h;
       rtx_material m;
@@ -398,11 +418,18 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
         cont = shade(A.S, A.max_depth, P, h, best >= 0, g, L, m);
       }
     }
+    RTX_STAMP(2)
     if (!cont) {
       store_radiance(A, slot, L);
       has = false;
     }
   }
+  RTX_STAMP(3)
+#if RTX_STAMPS
+  if (lane_id() == 0)
+    for (int i = 0; i < 4; i++) atomicAdd(&A.counters[24 + i], (unsigned long long)cyc[i]);
+#endif
+#undef RTX_STAMP
   flush_counters(A, c, segs, prims, COUNT);
 }
 
