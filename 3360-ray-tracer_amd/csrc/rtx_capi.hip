@@ -177,46 +177,73 @@ void prim_box(const rtx_prim& p, double lo[3], double hi[3]) {
 // BVH4 fast layout: the binary tree collapsed top-down.  Each F4Node starts from the binary
 // node's two children and repeatedly opens the slot with the largest surface area until it
 // holds four slots or nothing fits: an internal binary node opens into its two children, a
-// multi-primitive leaf (RTX_LEAF_SPLIT >= 1) into its primitives, each then a one-primitive
-// leaf slot with its own conservative box (prim_box), so the f32 slab test culls primitives
-// before their f64 test.  With RTX_LEAF_SPLIT >= 2 a multi-primitive leaf left in a slot
-// becomes a child F4Node of one-primitive slots.  Every slot keeps a box that contains all
-// hits its primitives can report, rounded outward, so the candidate set is unchanged.
+// leaf of 2-4 primitives into its primitives.  Every leaf slot of the result holds exactly
+// ONE primitive with its own conservative box (prim_box), so the f32 slab test culls
+// primitives before their f64 test and the kernel needs no per-slot counts: a leaf of
+// several primitives left in a slot becomes a child F4Node of one-primitive slots (and a leaf
+// of more than four, a small tree of them).  Empty slots carry an inverted box (lo = +inf,
+// hi = -inf) that no ray enters.  Every slot keeps a box that contains all hits its
+// primitives can report, rounded outward, so the candidate set is unchanged.
 // Returns the exact worst-case traversal stack depth (trace_fast4 pushes at most
-// `internal slots - 1` entries per visited node), or -1 when a leaf is too large for the
-// 16-bit slot count.
+// `internal slots - 1` entries per visited node).
 int build_fast4(const rtx_bvh_node* n, const rtx_prim* prims, std::vector<F4Node>& out) {
   out.clear();
   struct Slot {
-    int kind;  // 0 binary node, 1 primitive, 2 leaf-to-expand (binary leaf as an F4 child)
-    uint32_t id;
+    int kind;  // 0 binary node, 1 one primitive, 2 a primitive range emitted as a child node
+    uint32_t id, count;  // kind 0: node; kind 1: primitive; kind 2: first primitive, count
     double lo[3], hi[3];
   };
   auto node_slot = [&](uint32_t b) {
-    Slot s{0, b, {}, {}};
+    Slot s{0, b, 0, {}, {}};
     for (int a = 0; a < 3; a++) s.lo[a] = n[b].lo[a], s.hi[a] = n[b].hi[a];
+    if (n[b].is_leaf && n[b].right_count >= 2) s.kind = 2, s.id = n[b].left_first, s.count = n[b].right_count;
+    return s;
+  };
+  auto prim_slot = [&](uint32_t id) {
+    Slot s{1, id, 1, {}, {}};
+    prim_box(prims[id], s.lo, s.hi);
     return s;
   };
   auto area = [](const Slot& s) {
     const double dx = s.hi[0] - s.lo[0], dy = s.hi[1] - s.lo[1], dz = s.hi[2] - s.lo[2];
     return dx * dy + dy * dz + dz * dx;
   };
-  // number of slots a slot opens into (0: cannot open)
+  // the slots of the child node a kind-2 range becomes: its primitives (<= 4), else four
+  // contiguous sub-ranges with the union of their primitive boxes
+  auto range_slots = [&](uint32_t first, uint32_t count) {
+    std::vector<Slot> r;
+    if (count <= 4) {
+      for (uint32_t q = 0; q < count; q++) r.push_back(prim_slot(first + q));
+      return r;
+    }
+    const uint32_t per = (count + 3) / 4;
+    for (uint32_t g = first; g < first + count; g += per) {
+      const uint32_t k = std::min(per, first + count - g);
+      Slot sl{k == 1 ? 1 : 2, g, k, {INFINITY, INFINITY, INFINITY}, {-INFINITY, -INFINITY, -INFINITY}};
+      for (uint32_t q = 0; q < k; q++) {
+        double lo[3], hi[3];
+        prim_box(prims[g + q], lo, hi);
+        for (int a = 0; a < 3; a++) sl.lo[a] = std::min(sl.lo[a], lo[a]), sl.hi[a] = std::max(sl.hi[a], hi[a]);
+      }
+      r.push_back(sl);
+    }
+    return r;
+  };
+  // number of slots a slot opens into inside the current node (0: cannot open)
   auto fan = [&](const Slot& s) -> uint32_t {
-    if (s.kind != 0) return 0;
-    if (!n[s.id].is_leaf) return 2;
-    const uint32_t k = n[s.id].right_count;
-    return (RTX_LEAF_SPLIT >= 1 && k >= 2 && k <= 4) ? k : 0;
+    if (s.kind == 0) return n[s.id].is_leaf ? 0 : 2;
+    if (s.kind == 2) return s.count <= 4 ? s.count : 0;
+    return 0;
   };
   int need = 0;
-  bool ok = true;
   struct Item {
     std::vector<Slot> slots;
     int64_t parent_slot;
     int depth;
   };
   std::vector<Item> work;
-  work.push_back({{node_slot(n[0].left_first), node_slot(n[0].right_count)}, -1, 0});
+  if (n[0].is_leaf) work.push_back({range_slots(n[0].left_first, n[0].right_count), -1, 0});
+  else work.push_back({{node_slot(n[0].left_first), node_slot(n[0].right_count)}, -1, 0});
   while (!work.empty()) {
     Item it = std::move(work.back());
     work.pop_back();
@@ -234,61 +261,45 @@ int build_fast4(const rtx_bvh_node* n, const rtx_prim* prims, std::vector<F4Node
       if (pick < 0) break;
       const Slot b = slots[pick];
       std::vector<Slot> rep;
-      if (!n[b.id].is_leaf) {
-        rep = {node_slot(n[b.id].left_first), node_slot(n[b.id].right_count)};
-      } else {
-        for (uint32_t q = 0; q < n[b.id].right_count; q++) {
-          Slot ps{1, n[b.id].left_first + q, {}, {}};
-          prim_box(prims[ps.id], ps.lo, ps.hi);
-          rep.push_back(ps);
-        }
-      }
+      if (b.kind == 0) rep = {node_slot(n[b.id].left_first), node_slot(n[b.id].right_count)};
+      else rep = range_slots(b.id, b.count);
       slots.erase(slots.begin() + pick);
       slots.insert(slots.begin() + pick, rep.begin(), rep.end());
     }
-    for (Slot& sl : slots)  // leaves that stay whole: optionally one more level of prim slots
-      if (RTX_LEAF_SPLIT >= 2 && sl.kind == 0 && n[sl.id].is_leaf && n[sl.id].right_count >= 2 &&
-          n[sl.id].right_count <= 4)
-        sl.kind = 2;
     int internal = 0;
     for (const Slot& sl : slots) internal += (sl.kind == 2 || (sl.kind == 0 && !n[sl.id].is_leaf)) ? 1 : 0;
     const int child_depth = it.depth + std::max(0, internal - 1);
     need = std::max(need, child_depth);
     F4Node& f = out[me];
     for (int c = 0; c < 4; c++) {
-      if (c >= (int)slots.size()) {  // empty slot: empty leaf
-        f.child[c] = -1;
+      if (c >= (int)slots.size() || (slots[c].kind == 0 && n[slots[c].id].is_leaf && n[slots[c].id].right_count == 0)) {
+        f.child[c] = -1;  // empty slot: inverted box, never entered
+        f.lox[c] = f.loy[c] = f.loz[c] = INFINITY;
+        f.hix[c] = f.hiy[c] = f.hiz[c] = -INFINITY;
         continue;
       }
       const Slot& sl = slots[c];
       f.lox[c] = round_down(sl.lo[0]), f.loy[c] = round_down(sl.lo[1]), f.loz[c] = round_down(sl.lo[2]);
       f.hix[c] = round_up(sl.hi[0]), f.hiy[c] = round_up(sl.hi[1]), f.hiz[c] = round_up(sl.hi[2]);
-      uint32_t first = 0, count = 0;
-      if (sl.kind == 1) first = sl.id, count = 1;
-      else if (sl.kind == 0 && n[sl.id].is_leaf) first = n[sl.id].left_first, count = n[sl.id].right_count;
+      uint32_t first;
+      if (sl.kind == 1) first = sl.id;
+      else if (sl.kind == 0 && n[sl.id].is_leaf) first = n[sl.id].left_first;  // one-primitive binary leaf
       else continue;  // internal: patched when the child is emitted
-      if (count > 0xffffu) ok = false;
       f.child[c] = ~(int32_t)first;
-      f.counts[c >> 1] |= (count & 0xffffu) << (16 * (c & 1));
+      f.counts[c >> 1] |= 1u << (16 * (c & 1));
     }
     // push in reverse so children are laid out in slot order (pre-order)
     for (int c = (int)slots.size() - 1; c >= 0; c--) {
       const Slot& sl = slots[c];
       if (sl.kind == 2) {
-        std::vector<Slot> ps;
-        for (uint32_t q = 0; q < n[sl.id].right_count; q++) {
-          Slot p1{1, n[sl.id].left_first + q, {}, {}};
-          prim_box(prims[p1.id], p1.lo, p1.hi);
-          ps.push_back(p1);
-        }
-        work.push_back({std::move(ps), (int64_t)me * 4 + c, child_depth});
+        work.push_back({range_slots(sl.id, sl.count), (int64_t)me * 4 + c, child_depth});
       } else if (sl.kind == 0 && !n[sl.id].is_leaf) {
         work.push_back({{node_slot(n[sl.id].left_first), node_slot(n[sl.id].right_count)}, (int64_t)me * 4 + c,
                         child_depth});
       }
     }
   }
-  return ok ? need : -1;
+  return need;
 }
 
 // Fast-path tree of our own (RTX_FAST_TREE = 1): binned SAH on all three axes (32 bins)

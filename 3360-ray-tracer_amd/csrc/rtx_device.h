@@ -21,6 +21,9 @@
 #ifndef RTX_PRIM_PRELOAD
 #define RTX_PRIM_PRELOAD 1  // primitive record in one batch of loads before the kind branch
 #endif
+#ifndef RTX_NODE_LEAN
+#define RTX_NODE_LEAN 1  // BVH4 traversal without slot counts, slack folded into per-ray constants
+#endif
 #ifndef RTX_MERGED_SHADE
 #define RTX_MERGED_SHADE 1  // Sample() chains of the three materials in shared normalize/sqrt slots
 #endif
@@ -878,6 +881,127 @@ __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, doub
     } else {
       if (sp == 0) break;
       node = (int32_t)stk[(--sp) * stride];
+    }
+  }
+  t_best = closest;
+  return best;
+}
+
+// Lean variant of trace_fast4 (RTX_NODE_LEAN, default).  Relies on build_fast4's layout
+// guarantees: every leaf slot holds exactly one primitive and empty slots have an inverted
+// box, so the per-slot counts are not read.  The 1e-5 relative slack of the slab test is
+// folded into per-ray constants instead of two multiplies per slot:
+//   tn' = fma(plane, inv * (1 - s), nl * (1 - s)),  tf' = fma(plane, inv * (1 + s), nh * (1 + s))
+// i.e. (1 -/+ s) times each plane distance (monotone, so it commutes with the min/max and
+// with the clamp at 0); the extra rounding of the two products is < 2^-23 relative, far
+// inside s = 1e-5, and < 2^-23 |n0| absolute, inside the outward offset delta = 2^-20 |n0|
+// (see FRay4), so the test stays conservative.  Node loads use a 32-bit byte offset from the
+// (uniform) node-array base.
+struct FRay4L {
+  float iex, iey, iez, nex, ney, nez;  // entry planes: inverse and offset, scaled by (1 - s)
+  float ixx, ixy, ixz, nxx, nxy, nxz;  // exit planes: scaled by (1 + s)
+  uint32_t ox, oy, oz;                 // byte offset of the entry-plane array per axis (exit: ^ 16)
+};
+__device__ __forceinline__ FRay4L make_fray4l(V3 o, V3 d) {
+  FRay4 b;
+  fray4_axis_signed(o.x, d.x, 0, b.ix, b.nlx, b.nhx, b.ox);
+  fray4_axis_signed(o.y, d.y, 1, b.iy, b.nly, b.nhy, b.oy);
+  fray4_axis_signed(o.z, d.z, 2, b.iz, b.nlz, b.nhz, b.oz);
+  constexpr float lo = 0.99999f, hi = 1.00001f;
+  FRay4L r;
+  r.iex = b.ix * lo, r.iey = b.iy * lo, r.iez = b.iz * lo;
+  r.nex = b.nlx * lo, r.ney = b.nly * lo, r.nez = b.nlz * lo;
+  r.ixx = b.ix * hi, r.ixy = b.iy * hi, r.ixz = b.iz * hi;
+  r.nxx = b.nhx * hi, r.nxy = b.nhy * hi, r.nxz = b.nhz * hi;
+  r.ox = b.ox, r.oy = b.oy, r.oz = b.oz;
+  return r;
+}
+
+template <int STACK, bool COUNT>
+__device__ __forceinline__ int64_t trace_fast4_lean(const DScene& S, V3 o, V3 d, double tmin, double tmax,
+                                                    uint32_t* stk, int stride, Counters& cnt, double& t_best,
+                                                    int32_t& mat_best) {
+  int64_t best = -1;
+  double closest = tmax, t;
+  int32_t m;
+  mat_best = -1;
+  if (!S.use_bvh || S.froot_leaf) {
+    const int64_t n = S.use_bvh ? S.froot_count : S.n_prims;
+    for (int64_t i = 0; i < n; i++) {
+      if (COUNT) count_prim(cnt, S.prims + i);
+      if (prim_t(S.prims + i, S.has_tris, o, d, tmin, closest, t, m)) closest = t, best = i, mat_best = m;
+    }
+    t_best = closest;
+    return best;
+  }
+  const FRay4L r = make_fray4l(o, d);
+  const char* __restrict__ nbase = (const char*)S.f4nodes;
+  float tmax_f = f32_round_up(closest);
+  float tmax_x = tmax_f * 1.00001f;  // exit-side clamp with the slack folded in
+  int sp = 0;
+  uint32_t node = 0;
+  while (true) {
+    const uint32_t noff = node << 7;  // sizeof(F4Node) == 128
+    if (COUNT) {
+      cnt.nodes++;
+      if (first_active_lane()) cnt.wnodes++;
+    }
+    const int4 ch = *(const int4*)(nbase + (noff + 96u));
+    const float4 ex = *(const float4*)(nbase + (noff + r.ox)), fx = *(const float4*)(nbase + (noff + (r.ox ^ 16u)));
+    const float4 ey = *(const float4*)(nbase + (noff + r.oy)), fy = *(const float4*)(nbase + (noff + (r.oy ^ 16u)));
+    const float4 ez = *(const float4*)(nbase + (noff + r.oz)), fz = *(const float4*)(nbase + (noff + (r.oz ^ 16u)));
+    float tt[4];
+    int32_t cc[4] = {ch.x, ch.y, ch.z, ch.w};
+    uint32_t lmask = 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const float tn = fmaxf(fmaxf(fmaf(f4c(ex, c), r.iex, r.nex), fmaf(f4c(ey, c), r.iey, r.ney)),
+                             fmaxf(fmaf(f4c(ez, c), r.iez, r.nez), 0.0f));
+      const float tf = fminf(fminf(fmaf(f4c(fx, c), r.ixx, r.nxx), fmaf(f4c(fy, c), r.ixy, r.nxy)),
+                             fminf(fmaf(f4c(fz, c), r.ixz, r.nxz), tmax_x));
+      const bool hit = tn <= tf;
+      lmask |= (hit && cc[c] < 0) ? (1u << c) : 0u;
+      tt[c] = (hit && cc[c] >= 0) ? tn : __builtin_inff();
+    }
+    if (lmask) {
+      bool shrink = false;
+      while (lmask) {
+        const int c = __builtin_ctz(lmask);
+        lmask &= lmask - 1u;
+        const int32_t c01 = (c & 1) ? cc[1] : cc[0], c23 = (c & 1) ? cc[3] : cc[2];
+        const uint32_t cur = ~(uint32_t)((c & 2) ? c23 : c01);
+        if (COUNT) {
+          count_prim(cnt, S.prims + cur);
+          if (first_active_lane()) cnt.wprims++;
+        }
+        if (prim_t(S.prims + cur, S.has_tris, o, d, tmin, closest, t, m))
+          closest = t, best = (int64_t)cur, mat_best = m, shrink = true;
+      }
+      if (shrink) {
+        tmax_f = f32_round_up(closest);
+        tmax_x = tmax_f * 1.00001f;
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+          if (tt[c] > tmax_f) tt[c] = __builtin_inff();
+      }
+    }
+    cswap4(tt[0], cc[0], tt[1], cc[1]);
+    cswap4(tt[2], cc[2], tt[3], cc[3]);
+    cswap4(tt[0], cc[0], tt[2], cc[2]);
+    cswap4(tt[1], cc[1], tt[3], cc[3]);
+    cswap4(tt[1], cc[1], tt[2], cc[2]);
+    if (tt[0] != __builtin_inff()) {
+#pragma unroll
+      for (int c = 3; c >= 1; c--) {
+        if (tt[c] != __builtin_inff()) {
+          if (sp + 1 > STACK) __builtin_trap();
+          stk[(sp++) * stride] = (uint32_t)cc[c];
+        }
+      }
+      node = (uint32_t)cc[0];
+    } else {
+      if (sp == 0) break;
+      node = stk[(--sp) * stride];
     }
   }
   t_best = closest;

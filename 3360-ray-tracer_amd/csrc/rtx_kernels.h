@@ -24,9 +24,6 @@ constexpr int kBlock = 256;
 #ifndef RTX_TRACE_WAVES
 #define RTX_TRACE_WAVES 4  // min waves per SIMD for the trace kernels (<= 128 VGPRs; measured best)
 #endif
-#ifndef RTX_LEAF_SPLIT
-#define RTX_LEAF_SPLIT 2  // BVH4 (A/B r01: 2 = +15% C2, +24% bunny): 0 keep the reference's leaves, 1 open them into one-primitive slots, 2 also as child nodes
-#endif
 #ifndef RTX_FAST_TREE
 #define RTX_FAST_TREE 1  // A/B r01: +2% C2/bunny, +6% C5.  BVH4 source: 0 the reference's SAH tree, 1 our 3-axis SAH tree with 1-prim leaves
 #endif
@@ -122,7 +119,11 @@ template <int STACK, bool FAST, bool COUNT>
 __device__ __forceinline__ int64_t trace(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
                                          Counters& c, double& t_best, int32_t& mat_best) {
 #if RTX_BVH4
+#if RTX_NODE_LEAN
+  if (FAST) return trace_fast4_lean<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best, mat_best);
+#else
   if (FAST) return trace_fast4<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best, mat_best);
+#endif
   const int64_t b = trace_parity<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best);
 #else
   const int64_t b = FAST ? trace_fast<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best)
