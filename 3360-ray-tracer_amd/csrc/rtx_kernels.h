@@ -481,12 +481,13 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(PixelSoA px, const double
   px.conv[p] = conv;
 }
 
-// Fixed-spp megakernel accumulation: DefaultSampler sums GetPixel results in sample order.
-// Fixed-spp sum in sample order (the adds RecordSample does on `sum`).  One wave per 64
-// pixels: chunks of kAccChunk samples are staged through LDS with loads that cover each
-// pixel's contiguous run of 3*kAccChunk doubles, so a load instruction touches a few cache
-// lines instead of 64; each lane then adds its own pixel's samples in order.
-constexpr int kAccWave = 64, kAccChunk = 8, kAccPitch = 3 * kAccChunk + 1;  // odd pitch: 2-way LDS banks
+// Fixed-spp accumulation: the sum RecordSample (and DefaultSampler) forms, in sample order.
+// One wave per 64 consecutive pixels, whose radiance runs are one contiguous region of Lbuf
+// (pixel-major slots).  Chunks of kAccChunk samples are staged through LDS: the wave reads
+// each pixel's contiguous run of 3 * kAccChunk doubles with 16-byte loads (8-byte loads when
+// the runs are not 16-byte aligned, i.e. K odd, or for a short last chunk), all issued before
+// the first LDS store, then each lane adds its own pixel's samples in order.
+constexpr int kAccWave = 64, kAccChunk = 16, kAccPitch = 3 * kAccChunk + 1;  // odd pitch: spread LDS banks
 __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const double* __restrict__ L, int64_t npix,
                                                              int K) {
   __shared__ double st[kAccWave * kAccPitch];
@@ -494,14 +495,31 @@ __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const 
   const int64_t p0 = (int64_t)blockIdx.x * kAccWave;
   const int npx = (int)std::min<int64_t>(kAccWave, npix - p0);
   const int64_t p = p0 + t;
+  const double* __restrict__ base = L + p0 * 3 * (int64_t)K;
   double sum[3] = {0, 0, 0};
   if (t < npx)
     for (int c = 0; c < 3; c++) sum[c] = px.sum[c * npix + p];
   for (int k0 = 0; k0 < K; k0 += kAccChunk) {
-    const int kc = std::min(kAccChunk, K - k0), run = 3 * kc, total = npx * run;
-    for (int e = t; e < total; e += kAccWave) {
-      const int q = e / run, j = e - q * run;
-      st[q * kAccPitch + j] = L[(p0 + q) * 3 * (int64_t)K + 3 * k0 + j];
+    const int kc = std::min(kAccChunk, K - k0);
+    if (kc == kAccChunk && (K & 1) == 0) {
+      constexpr int PP = 3 * kAccChunk / 2;  // 16-byte pieces per pixel run
+      double2 v[PP];
+#pragma unroll
+      for (int i = 0; i < PP; i++) {
+        const int e = t + kAccWave * i, q = e / PP, j = e - q * PP;
+        if (q < npx) v[i] = *(const double2*)(base + (int64_t)q * 3 * K + 3 * k0 + 2 * j);
+      }
+#pragma unroll
+      for (int i = 0; i < PP; i++) {
+        const int e = t + kAccWave * i, q = e / PP, j = e - q * PP;
+        if (q < npx) st[q * kAccPitch + 2 * j] = v[i].x, st[q * kAccPitch + 2 * j + 1] = v[i].y;
+      }
+    } else {
+      const int run = 3 * kc, total = npx * run;
+      for (int e = t; e < total; e += kAccWave) {
+        const int q = e / run, j = e - q * run;
+        st[q * kAccPitch + j] = base[(int64_t)q * 3 * K + 3 * k0 + j];
+      }
     }
     __syncthreads();
     if (t < npx)

@@ -149,15 +149,13 @@ def main():
     if os.path.exists(tf):
         prof = json.load(open(tf))
         traffic = prof.get("hbm_bytes_per_launch")
-        if prof.get("valu_insts_per_launch"):
-            # VALU issue (the kernel's actual limiter; the scene is L2/MALL-resident): wave64
-            # VALU instructions per launch from the committed PMC profile of this build, over
-            # the live launch time; peak = 1 wave-instruction / 2 cycles / SIMD (SIMD-32,
-            # MI355X_MICROARCH.md) x 1024 SIMDs x 2.4 GHz
-            v_rate = prof["valu_insts_per_launch"] / avg_launch_s
-            v_peak = 1024 * 2.4e9 / 2
-            valu = {"achieved": v_rate, "peak": v_peak, "unit": "wave-instr/s", "frac": v_rate / v_peak,
-                    "source": prof.get("source")}
+        if prof.get("valu_busy") is not None:
+            # The kernel's actual limiter is VALU issue (the scene is L2/MALL-resident): the
+            # fraction of SIMD cycles that issue a VALU instruction, from the committed PMC
+            # profile of this build (SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)).
+            valu = {"busy_frac": prof["valu_busy"], "insts_per_launch": prof.get("valu_insts_per_launch"),
+                    "source": prof.get("source"),
+                    "note": "fraction of SIMD cycles issuing VALU (PMC, profiled run of this build)"}
 
     out = None
     if rank == 0:
@@ -215,14 +213,16 @@ def cpu_baseline(rtx, dev, host, cam, preset, spp, depth, args):
         host.write(path)
         s = orc.Scene(path)
         cfg = orc.camera_preset(preset)
-        # probe on a small centre crop, then size the timed sample to ~10 s of CPU work
-        # (capped at the whole frame): full-width bands of rows around the image centre
-        probe = (0, H // 2 - 2, W, 4)
-        t0 = time.perf_counter()
-        s.render(cfg, W, spp, depth, args.seed, adaptive=0, rng="philox", mode="per_pixel", tile=probe,
-                 threads=threads)
-        per_row = (time.perf_counter() - t0) / 4
-        ch = int(max(4, min(H, 10.0 / max(per_row, 1e-6))))
+        # probe on a small centre crop (twice: the first call also starts the thread pool),
+        # then size the timed sample to ~10 s of wall time on `threads` cores, capped at the
+        # whole frame: full-width bands of rows around the image centre
+        probe = (0, H // 2 - 4, W, 8)
+        for _ in range(2):
+            t0 = time.perf_counter()
+            s.render(cfg, W, spp, depth, args.seed, adaptive=0, rng="philox", mode="per_pixel", tile=probe,
+                     threads=threads)
+            per_row = (time.perf_counter() - t0) / 8
+        ch = int(max(8, min(H, 10.0 / max(per_row, 1e-6))))
         cw = W
         tile = (0, max(0, H // 2 - ch // 2), cw, ch)
         t0 = time.perf_counter()
@@ -232,8 +232,9 @@ def cpu_baseline(rtx, dev, host, cam, preset, spp, depth, args):
     gpu, _, _ = dev.render(cam, spp, depth, seed=args.seed, adaptive=False, tile=tile, mode="wavefront",
                            precision="parity")
     rms = float(np.sqrt(np.mean((gpu - ref.reshape(-1, 3)) ** 2)))
+    what = "the whole" if ch == H else f"centre band {cw}x{ch} of the same"
     base = {"value": st["rays"] / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"centre band {cw}x{ch} of the same {W}x{H} frame, {spp} spp, depth {depth}, "
+            "sample": f"{what} {W}x{H} frame, {spp} spp, depth {depth}, fixed spp, "
                       f"{st['rays']} segments in {dt:.1f}s (oracle/rtx_oracle.cc, OpenMP, philox)"}
     return base, rms
 

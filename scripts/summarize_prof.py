@@ -50,10 +50,17 @@ def main():
             n_f = len(launches[(k, "FETCH_SIZE")])
             n_w = len(launches[(k, "WRITE_SIZE")])
             per = v["FETCH_SIZE"] * 2 * 1024 / n_f + v["WRITE_SIZE"] * 1024 / n_w
-            valu = None
+            valu = busy = None
             if "SQ_INSTS_VALU" in v:
                 valu = v["SQ_INSTS_VALU"] / max(1, len(launches[(k, "SQ_INSTS_VALU")]))
-            t = {"kernel": k, "hbm_bytes_per_launch": per, "valu_insts_per_launch": valu,
+            if "SQ_ACTIVE_INST_VALU" in v and "GRBM_GUI_ACTIVE" in v:
+                # fraction of SIMD cycles issuing VALU: SQ_ACTIVE_INST_VALU counts quad-cycles per
+                # wave (summed over waves; one wave issues VALU per SIMD per cycle), GRBM_GUI_ACTIVE
+                # is summed over the 8 XCDs (MI355X_MICROARCH.md, cycle constants)
+                act = v["SQ_ACTIVE_INST_VALU"] / max(1, len(launches[(k, "SQ_ACTIVE_INST_VALU")]))
+                cyc = v["GRBM_GUI_ACTIVE"] / max(1, len(launches[(k, "GRBM_GUI_ACTIVE")])) / 8
+                busy = 4 * act / (1024 * cyc)
+            t = {"kernel": k, "hbm_bytes_per_launch": per, "valu_insts_per_launch": valu, "valu_busy": busy,
                  "fetch_kib_total": v["FETCH_SIZE"],
                  "write_kib_total": v["WRITE_SIZE"], "launches_fetch_pass": n_f, "launches_write_pass": n_w,
                  "source": f"profiles/{rnd}/pmc_{tag}.json", "correction": "FETCH_SIZE x2 (gfx950)"}
