@@ -79,6 +79,8 @@ struct rtx_scene {
   DScene S{};
   int stack_parity = 32, stack_fast = 32;
   bool fast_ok = false;  // RTX_PREC_FAST available (BVH with an internal root)
+  int park = -1;         // persistent fast schedule: -1 not yet timed, 0 plain kernel, 1 PARK kernel
+  DevBuf calib_rgb;      // output of the schedule-timing renders
   int64_t n_nodes = 0;
   // render workspace (grow-only)
   DevBuf px_sum, px_mean, px_m2, px_samples, px_conv, lbuf, queue[2], counters, out_rgb, out_spp, rays, hits;
@@ -90,7 +92,7 @@ struct rtx_scene {
     (void)hipSetDevice(device);
     for (DevBuf* b : {&nodes, &prims, &mats, &texs, &images, &fnodes, &px_sum, &px_mean, &px_m2, &px_samples,
                       &px_conv, &lbuf, &queue[0], &queue[1], &counters, &out_rgb, &out_spp, &rays, &hits, &p3_scratch,
-                      &p3_body})
+                      &p3_body, &calib_rgb})
       b->release();
     for (auto& t : texels) t.release();
     for (auto& e : ev)
@@ -463,6 +465,7 @@ struct Launch {
   hipStream_t s;
   int stack;
   bool fast, count;
+  bool park = false;  // persistent: the PARK kernel (parked traversals), chosen per scene
 };
 
 template <int STACK, bool FAST, bool COUNT>
@@ -476,11 +479,12 @@ int run_extend(const Launch& L, const RenderArgs& A, const PathQueue& q, const u
   return RTX_OK;
 }
 
-template <int STACK, bool FAST, bool COUNT, bool SCATTER>
+template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK>
 int run_persistent(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
   const size_t lds = STACK * kBlock * sizeof(uint32_t);
-  const int grid = persistent_grid(L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER>, lds);
-  hipLaunchKernelGGL((k_persistent<STACK, FAST, COUNT, SCATTER>), dim3(grid), dim3(kBlock), lds, L.s, A, next_slot);
+  const int grid = persistent_grid(L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK>, lds);
+  hipLaunchKernelGGL((k_persistent<STACK, FAST, COUNT, SCATTER, PARK>), dim3(grid), dim3(kBlock), lds, L.s, A,
+                     next_slot);
   HIPC(hipGetLastError());
   return RTX_OK;
 }
@@ -494,16 +498,21 @@ int extend(const Launch& L, const RenderArgs& A, const PathQueue& q, const unsig
   if (L.fast) return L.count ? extend_s<true, true>(L, A, q, c, n) : extend_s<true, false>(L, A, q, c, n);
   return L.count ? extend_s<false, true>(L, A, q, c, n) : extend_s<false, false>(L, A, q, c, n);
 }
-template <bool FAST, bool COUNT, bool SCATTER>
+template <bool FAST, bool COUNT, bool SCATTER, bool PARK>
 int persist_s(const Launch& L, const RenderArgs& A, unsigned long long* ns) {
-  return L.stack == 32 ? run_persistent<32, FAST, COUNT, SCATTER>(L, A, ns)
-                       : run_persistent<64, FAST, COUNT, SCATTER>(L, A, ns);
+  return L.stack == 32 ? run_persistent<32, FAST, COUNT, SCATTER, PARK>(L, A, ns)
+                       : run_persistent<64, FAST, COUNT, SCATTER, PARK>(L, A, ns);
 }
 template <bool SCATTER>
 int persist_m(const Launch& L, const RenderArgs& A, unsigned long long* ns) {
-  if (L.fast) return L.count ? persist_s<true, true, SCATTER>(L, A, ns) : persist_s<true, false, SCATTER>(L, A, ns);
-  return L.count ? persist_s<false, true, SCATTER>(L, A, ns) : persist_s<false, false, SCATTER>(L, A, ns);
+  if (L.fast && L.park && !SCATTER && RTX_PARK > 0)
+    return L.count ? persist_s<true, true, SCATTER, true>(L, A, ns) : persist_s<true, false, SCATTER, true>(L, A, ns);
+  if (L.fast)
+    return L.count ? persist_s<true, true, SCATTER, false>(L, A, ns) : persist_s<true, false, SCATTER, false>(L, A, ns);
+  return L.count ? persist_s<false, true, SCATTER, false>(L, A, ns) : persist_s<false, false, SCATTER, false>(L, A, ns);
 }
+
+int time_park_schedule(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm);
 
 }  // namespace
 
@@ -774,6 +783,15 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
   hipStream_t s = stream ? (hipStream_t)stream : sc->stream;
   const bool fast = prm->precision == RTX_PREC_FAST && sc->fast_ok;
   Launch L{sc, s, fast ? sc->stack_fast : sc->stack_parity, fast, (prm->flags & RTX_FLAG_COUNT) != 0};
+  if (fast && prm->mode == RTX_MODE_PERSISTENT && RTX_PARK > 0) {
+    if (prm->flags & RTX_FLAG_PARK) L.park = true;
+    else if (prm->flags & RTX_FLAG_NO_PARK) L.park = false;
+    else {
+      int rc;
+      if (sc->park < 0 && (rc = time_park_schedule(sc, cam, prm))) return rc;
+      L.park = sc->park == 1;
+    }
+  }
 
   // samples in flight per pixel (group size K)
   int K = prm->samples_per_group;
@@ -924,6 +942,7 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
     unsigned long long h[8];
     HIPC(hipMemcpy(h, cnt, sizeof h, hipMemcpyDeviceToHost));
     stats->rays_total = h[0];
+    stats->parked = L.park ? 1 : 0;
     stats->rays_primary = h[1];
     stats->paths = h[1];
     stats->kernel_ms = ms;
@@ -936,6 +955,15 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
     stats->tri_tests = h[6];
     stats->sphere_tests = h[7];
     stats->node_bytes = (L.fast && RTX_BVH4) ? sizeof(F4Node) : (L.fast ? sizeof(FNode) : sizeof(rtx_bvh_node));
+#if RTX_TAILHIST
+    if (h[4]) {
+      unsigned long long th[6];
+      HIPC(hipMemcpy(th, cnt + 40, sizeof th, hipMemcpyDeviceToHost));
+      fprintf(stderr, "rtx tail: node-loop wave iterations %llu; fraction with <=1/2/4/8/16/32 active lanes:", h[4]);
+      for (int i = 0; i < 6; i++) fprintf(stderr, " %.4f", (double)th[i] / (double)h[4]);
+      fprintf(stderr, "\n");
+    }
+#endif
 #if RTX_STAMPS
     unsigned long long st[4];
     HIPC(hipMemcpy(st, cnt + 24, sizeof st, hipMemcpyDeviceToHost));
@@ -1050,3 +1078,34 @@ int rtx_write_ppm(const char* path, const double* rgb, int32_t w, int32_t h) {
 }
 
 }  // extern "C"
+
+namespace {
+
+// Which persistent fast schedule suits this scene: the PARK kernel wins where a few lanes
+// walk long after the rest of their wave (dense meshes: the bunny, +14..18 %) and loses where
+// shading dominates (sphere scenes, -5..-10 %), see DESIGN.md.  Both produce identical
+// results, so the choice is timing only: the first persistent fast render of a scene renders
+// a centre tile of 1/16 of its pixels with each kernel (twice each; the faster second run
+// counts) and keeps the one with the higher segment rate for the scene.
+int time_park_schedule(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm) {
+  rtx_render_params q = *prm;
+  q.stripe_rows = q.stripe_index = q.stripe_count = 0;
+  q.w = std::max(1, cam->image_width / 4), q.h = std::max(1, cam->image_height / 4);
+  q.x0 = (cam->image_width - q.w) / 2, q.y0 = (cam->image_height - q.h) / 2;
+  q.flags = prm->flags & ~(RTX_FLAG_COUNT | RTX_FLAG_PARK | RTX_FLAG_NO_PARK);
+  int rc;
+  if ((rc = sc->calib_rgb.reserve((size_t)q.w * q.h * 3 * sizeof(double)))) return rc;
+  double rate[2] = {0, 0};
+  for (int rep = 0; rep < 2; rep++)
+    for (int k = 0; k < 2; k++) {
+      rtx_render_params r = q;
+      r.flags |= k ? RTX_FLAG_PARK : RTX_FLAG_NO_PARK;
+      rtx_stats st{};
+      if ((rc = rtx_render_device(sc, cam, &r, sc->calib_rgb.as<double>(), nullptr, &st, nullptr))) return rc;
+      rate[k] = st.hot_kernel_ms > 0 ? (double)st.rays_total / st.hot_kernel_ms : 0.0;
+    }
+  sc->park = rate[1] > 1.02 * rate[0] ? 1 : 0;
+  return RTX_OK;
+}
+
+}  // namespace

@@ -21,6 +21,9 @@
 #ifndef RTX_PRIM_PRELOAD
 #define RTX_PRIM_PRELOAD 1  // primitive record in one batch of loads before the kind branch
 #endif
+#ifndef RTX_TAILHIST
+#define RTX_TAILHIST 0  // diagnostic build: histogram of active lanes per node-loop iteration
+#endif
 #ifndef RTX_NODE_LEAN
 #define RTX_NODE_LEAN 1  // BVH4 traversal without slot counts, slack folded into per-ray constants
 #endif
@@ -509,6 +512,9 @@ struct Counters {
   uint32_t nodes, prims;  // lane-level node visits / primitive tests
   uint32_t wnodes, wprims;  // wave-level loop iterations (counted by the first active lane)
   uint32_t tris, sphs;      // primitive tests by kind (rects = prims - tris - sphs)
+#if RTX_TAILHIST
+  uint32_t tail[6];  // diagnostic: node-loop wave iterations with <= 1, 2, 4, 8, 16, 32 active lanes
+#endif
 };
 __device__ __forceinline__ void count_prim(Counters& c, const rtx_prim* P) {
   c.prims++;
@@ -917,34 +923,52 @@ __device__ __forceinline__ FRay4L make_fray4l(V3 o, V3 d) {
   return r;
 }
 
+// Resumable form of the lean traversal.  TravState is everything a lane needs to continue
+// a traversal later: the stack itself stays in the lane's LDS column, and the per-ray slab
+// constants are recomputed from (o, d).  trace4_run() walks until the ray is done (true) or,
+// when park_at >= 0, until at most park_at lanes of the wave are still walking at the top of
+// a node iteration (false: the lane is parked with its state intact).  A parked ray continues
+// exactly where it stopped, so the sequence of node visits and primitive tests — and the
+// result — is the same as one uninterrupted walk.
+struct TravState {
+  uint32_t node;
+  int32_t sp;
+  double closest;
+  int32_t best;  // leaf-order primitive index or -1
+  int32_t mat;   // its material id
+  float tmax_f;  // f32_round_up(closest)
+};
+__device__ __forceinline__ void trav_init(TravState& ts, double tmax) {
+  ts.node = 0, ts.sp = 0, ts.closest = tmax, ts.best = -1, ts.mat = -1;
+  ts.tmax_f = f32_round_up(tmax);
+}
+
 template <int STACK, bool COUNT>
-__device__ __forceinline__ int64_t trace_fast4_lean(const DScene& S, V3 o, V3 d, double tmin, double tmax,
-                                                    uint32_t* stk, int stride, Counters& cnt, double& t_best,
-                                                    int32_t& mat_best) {
-  int64_t best = -1;
-  double closest = tmax, t;
-  int32_t m;
-  mat_best = -1;
-  if (!S.use_bvh || S.froot_leaf) {
-    const int64_t n = S.use_bvh ? S.froot_count : S.n_prims;
-    for (int64_t i = 0; i < n; i++) {
-      if (COUNT) count_prim(cnt, S.prims + i);
-      if (prim_t(S.prims + i, S.has_tris, o, d, tmin, closest, t, m)) closest = t, best = i, mat_best = m;
-    }
-    t_best = closest;
-    return best;
-  }
+__device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double tmin, uint32_t* stk, int stride,
+                                           Counters& cnt, TravState& ts, int park_at) {
   const FRay4L r = make_fray4l(o, d);
   const char* __restrict__ nbase = (const char*)S.f4nodes;
-  float tmax_f = f32_round_up(closest);
+  double closest = ts.closest, t;
+  int32_t best = ts.best, mat_best = ts.mat, m;
+  float tmax_f = ts.tmax_f;
   float tmax_x = tmax_f * 1.00001f;  // exit-side clamp with the slack folded in
-  int sp = 0;
-  uint32_t node = 0;
+  int sp = ts.sp;
+  uint32_t node = ts.node;
+  bool done = true;
   while (true) {
+    if (park_at >= 0 && __popcll(__ballot(1)) <= park_at) {
+      done = false;
+      break;
+    }
     const uint32_t noff = node << 7;  // sizeof(F4Node) == 128
     if (COUNT) {
       cnt.nodes++;
       if (first_active_lane()) cnt.wnodes++;
+#if RTX_TAILHIST
+      const int act = __popcll(__ballot(1));
+      if (first_active_lane())
+        for (int i = 0; i < 6; i++) cnt.tail[i] += act <= (1 << i) ? 1u : 0u;
+#endif
     }
     const int4 ch = *(const int4*)(nbase + (noff + 96u));
     const float4 ex = *(const float4*)(nbase + (noff + r.ox)), fx = *(const float4*)(nbase + (noff + (r.ox ^ 16u)));
@@ -975,7 +999,7 @@ __device__ __forceinline__ int64_t trace_fast4_lean(const DScene& S, V3 o, V3 d,
           if (first_active_lane()) cnt.wprims++;
         }
         if (prim_t(S.prims + cur, S.has_tris, o, d, tmin, closest, t, m))
-          closest = t, best = (int64_t)cur, mat_best = m, shrink = true;
+          closest = t, best = (int32_t)cur, mat_best = m, shrink = true;
       }
       if (shrink) {
         tmax_f = f32_round_up(closest);
@@ -1004,8 +1028,37 @@ __device__ __forceinline__ int64_t trace_fast4_lean(const DScene& S, V3 o, V3 d,
       node = stk[(--sp) * stride];
     }
   }
+  ts.node = node, ts.sp = sp, ts.closest = closest, ts.best = best, ts.mat = mat_best, ts.tmax_f = tmax_f;
+  return done;
+}
+
+// Linear closest hit over the whole primitive list (scene::Scene::Hit, scene.h:47-61), or the
+// fast BVH's single-leaf root.
+__device__ __forceinline__ int64_t trace_flat(const DScene& S, V3 o, V3 d, double tmin, double tmax, Counters& cnt,
+                                              bool count, double& t_best, int32_t& mat_best) {
+  int64_t best = -1;
+  double closest = tmax, t;
+  int32_t m;
+  mat_best = -1;
+  const int64_t n = S.use_bvh ? S.froot_count : S.n_prims;
+  for (int64_t i = 0; i < n; i++) {
+    if (count) count_prim(cnt, S.prims + i);
+    if (prim_t(S.prims + i, S.has_tris, o, d, tmin, closest, t, m)) closest = t, best = i, mat_best = m;
+  }
   t_best = closest;
   return best;
+}
+
+template <int STACK, bool COUNT>
+__device__ __forceinline__ int64_t trace_fast4_lean(const DScene& S, V3 o, V3 d, double tmin, double tmax,
+                                                    uint32_t* stk, int stride, Counters& cnt, double& t_best,
+                                                    int32_t& mat_best) {
+  if (!S.use_bvh || S.froot_leaf) return trace_flat(S, o, d, tmin, tmax, cnt, COUNT, t_best, mat_best);
+  TravState ts;
+  trav_init(ts, tmax);
+  trace4_run<STACK, COUNT>(S, o, d, tmin, stk, stride, cnt, ts, -1);
+  t_best = ts.closest, mat_best = ts.mat;
+  return ts.best;
 }
 
 // ---------------------------------------------------------------------------------------

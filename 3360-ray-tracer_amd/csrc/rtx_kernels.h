@@ -148,6 +148,9 @@ __device__ __forceinline__ void flush_counters(const RenderArgs& A, const Counte
     atomicAdd(&A.counters[5], (unsigned long long)c.wprims);
     atomicAdd(&A.counters[6], (unsigned long long)c.tris);
     atomicAdd(&A.counters[7], (unsigned long long)c.sphs);
+#if RTX_TAILHIST
+    for (int i = 0; i < 6; i++) atomicAdd(&A.counters[40 + i], (unsigned long long)c.tail[i]);
+#endif
   }
   if (segs) atomicAdd(&A.counters[0], (unsigned long long)segs);
   if (prims) atomicAdd(&A.counters[1], (unsigned long long)prims);
@@ -286,12 +289,15 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in,
 // (miss, emitter, absorption, Russian roulette) are immediately given a new primary —
 // the per-wave __ballot of idle lanes is the active-ray compaction.
 // ---------------------------------------------------------------------------------------
+#ifndef RTX_PARK
+#define RTX_PARK 16  // persistent (PARK kernel): park traversals once at most this many lanes still walk (A/B r01: 16 best for the bunny; 0: no PARK kernel)
+#endif
 #ifndef RTX_CHUNK
 #define RTX_CHUNK 256  // persistent: slots taken per atomic on the global slot counter
 #endif
 constexpr int kChunk = RTX_CHUNK;
 
-template <int STACK, bool FAST, bool COUNT, bool SCATTER>
+template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK>
 __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderArgs A, unsigned long long* next_slot) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* stk = lds + threadIdx.x;
@@ -307,6 +313,14 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
   P.depth = 0;
   uint32_t slot = 0;           // < nslots <= 2^32 - 1 (host check)
   uint32_t pix = 0, smp = 0;  // RNG identity of the lane's path: global pixel, sample
+  // A traversal still running when at most RTX_PARK lanes of the wave are left walking is
+  // parked (trace4_run) and resumed in the next segment round, so the wave goes on to shade
+  // the finished lanes instead of idling behind a few long walks.
+  // (PARK instantiation only: the host picks it per scene, see rtx_render_device.)
+  constexpr bool kPark = PARK && FAST && !SCATTER && RTX_BVH4 && RTX_NODE_LEAN && RTX_PARK > 0;
+  const bool park_ok = kPark && A.S.use_bvh && !A.S.froot_leaf;
+  bool parked = false;
+  TravState trs;
 #if RTX_STAMPS
   uint64_t cyc[4] = {0, 0, 0, 0};
   uint64_t ts = __builtin_amdgcn_s_memtime();
@@ -381,7 +395,21 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
     } else {
       double tb;
       int32_t bmat;
-      const int64_t best = trace<STACK, FAST, COUNT>(A.S, P.o, P.d, tmin, kInf, stk, c, tb, bmat);
+      int64_t best;
+      if (kPark && park_ok) {
+        const int active = __popcll(__ballot(1));  // lanes tracing this round
+        if (!parked) trav_init(trs, kInf);
+        // parking only when some lane of this round finishes first: every round makes progress
+        const bool done = trace4_run<STACK, COUNT>(A.S, P.o, P.d, tmin, stk, kBlock, c, trs,
+                                                   active > RTX_PARK ? RTX_PARK : -1);
+        parked = !done;
+        if (parked) continue;
+        best = trs.best, tb = trs.closest, bmat = trs.mat;
+      } else if (kPark) {  // no BVH, or its root is a leaf
+        best = trace_flat(A.S, P.o, P.d, tmin, kInf, c, COUNT, tb, bmat);
+      } else {
+        best = trace<STACK, FAST, COUNT>(A.S, P.o, P.d, tmin, kInf, stk, c, tb, bmat);
+      }
       RTX_STAMP(1)
       segs++;
       Hit h;

@@ -91,7 +91,7 @@ class Stats(C.Structure):
                 ("kernel_ms", C.c_double), ("hot_kernel_ms", C.c_double), ("hot_launches", C.c_uint64),
                 ("node_visits", C.c_uint64), ("prim_tests", C.c_uint64),
                 ("node_bytes", C.c_uint64), ("wave_node_iters", C.c_uint64), ("wave_prim_iters", C.c_uint64),
-                ("tri_tests", C.c_uint64), ("sphere_tests", C.c_uint64)]
+                ("tri_tests", C.c_uint64), ("sphere_tests", C.c_uint64), ("parked", C.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -274,13 +274,13 @@ class DeviceScene:
 
     def render(self, cam, spp, max_depth, seed=1234, adaptive=True, mode="wavefront", precision="parity",
                tile=None, stripes=None, samples_per_group=0, min_spp=16, rel_threshold=float(np.float32(0.05)),
-               count=False):
+               count=False, schedule=None):
         p = RenderParams()
         p.spp, p.max_depth, p.adaptive = spp, max_depth, int(bool(adaptive))
         p.min_spp, p.rel_threshold, p.seed = min_spp, rel_threshold, seed
         p.mode, p.precision = MODES[mode], PRECISIONS[precision]
         p.samples_per_group = samples_per_group
-        p.flags = 1 if count else 0
+        p.flags = (1 if count else 0) | {None: 0, "park": 2, "plain": 4}[schedule]
         if stripes is not None:
             p.stripe_rows, p.stripe_index, p.stripe_count = stripes
         elif tile is not None:

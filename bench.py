@@ -177,6 +177,7 @@ def main():
                        "scene_prims": int(host.desc().n_prims), "bvh_nodes": int(host.desc().n_nodes),
                        "mode": args.mode, "precision": args.precision, "spp_total": total_spp,
                        "pixels_per_rank": int(npix), "stripe_rows": STRIPE_ROWS if world > 1 else None,
+                       "schedule": "park" if stats[-1].get("parked") else "plain",
                        "parallelism": f"tile-split x{world} (interleaved row stripes, no collectives)"},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,

@@ -41,7 +41,7 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 2  /* 2: rtx_stats.node_bytes */
+#define RTX_ABI_VERSION 3  /* 2: rtx_stats.node_bytes; 3: rtx_stats.parked, RTX_FLAG_PARK / NO_PARK */
 
 enum {
   RTX_OK = 0,
@@ -194,7 +194,12 @@ typedef struct {
 } rtx_render_params;
 
 enum {
-  RTX_FLAG_COUNT = 1 /* count BVH node visits / primitive tests (diagnostic build of the kernel) */
+  RTX_FLAG_COUNT = 1,  /* count BVH node visits / primitive tests (diagnostic build of the kernel) */
+  /* RTX_MODE_PERSISTENT + RTX_PREC_FAST schedule (results are identical either way): by
+     default the first such render of a scene times both on a centre tile and keeps the
+     faster for the scene; these flags force one */
+  RTX_FLAG_PARK = 2,   /* park long traversals and resume them in the next segment round */
+  RTX_FLAG_NO_PARK = 4 /* every traversal runs to completion within its round */
 };
 
 typedef struct {
@@ -211,6 +216,7 @@ typedef struct {
   uint64_t wave_prim_iters; /*   = node_visits / (64 * wave_node_iters)); primitive-loop iterations per wave */
   uint64_t tri_tests;       /* with RTX_FLAG_COUNT: triangle / sphere tests among prim_tests (rest: rects) */
   uint64_t sphere_tests;
+  uint64_t parked;          /* 1: the persistent fast schedule that parks long traversals ran */
 } rtx_stats;
 
 /* ---- entry points ------------------------------------------------------------------ */

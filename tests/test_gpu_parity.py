@@ -260,3 +260,26 @@ def test_persistent_schedule_equals_wavefront(rtx_mod, dev_scenes, scene, preset
     b, sb, _ = dev_scenes(scene).render(cam, spp, depth, seed=8, adaptive=adaptive, mode="persistent",
                                         precision=precision)
     assert np.array_equal(a, b) and np.array_equal(sa, sb)
+
+
+@pytest.mark.parametrize("scene,preset,w,spp,depth,adaptive", [("bunny", "c3_bunny", 64, 8, 20, 0),
+                                                               ("final", "c2_final", 64, 8, 50, 0),
+                                                               ("final", "c2_final", 48, 6, 50, 1),
+                                                               ("cornell", "cornell", 40, 8, 50, 0),
+                                                               ("mixed", "c5_mixed", 48, 4, 50, 0)])
+def test_parked_traversal_schedule_is_bit_identical(rtx_mod, dev_scenes, scene, preset, w, spp, depth, adaptive):
+    """The persistent fast kernel that parks long traversals and resumes them in the next
+    segment round (RTX_FLAG_PARK) walks every ray through the same node and primitive
+    sequence as the plain kernel: pixels, sample counts and segment counts are identical, and
+    so is the automatically timed per-scene choice."""
+    cam = rtx_mod.camera(rtx_mod.camera_config(preset, width=w))
+    d = dev_scenes(scene)
+    out = {}
+    for sched in ("plain", "park", None):
+        out[sched] = d.render(cam, spp, depth, seed=5, adaptive=adaptive, mode="persistent", precision="fast",
+                              schedule=sched)
+    (a, sa, sta), (b, sb, stb), (c, sc, stc) = out["plain"], out["park"], out[None]
+    fast4 = stb["node_bytes"] == 128  # the BVH4 fast path exists (a flat list renders in parity precision)
+    assert sta["parked"] == 0 and stb["parked"] == (1 if fast4 else 0) and stc["parked"] in (0, 1)
+    assert np.array_equal(a, b) and np.array_equal(sa, sb) and sta["rays_total"] == stb["rays_total"]
+    assert np.array_equal(a, c) and np.array_equal(sa, sc)
