@@ -515,7 +515,13 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(PixelSoA px, const double
 // each pixel's contiguous run of 3 * kAccChunk doubles with 16-byte loads (8-byte loads when
 // the runs are not 16-byte aligned, i.e. K odd, or for a short last chunk), all issued before
 // the first LDS store, then each lane adds its own pixel's samples in order.
-constexpr int kAccWave = 64, kAccChunk = 16, kAccPitch = 3 * kAccChunk + 1;  // odd pitch: spread LDS banks
+#ifndef RTX_ACC_CHUNK
+#define RTX_ACC_CHUNK 4  // samples per LDS-staged chunk of the fixed-spp accumulate (4 > 8 > 16, ab_acc_pipe)
+#endif
+#ifndef RTX_ACC_PIPE
+#define RTX_ACC_PIPE 1  // accumulate: the next chunk's loads are in flight while the current one is summed
+#endif
+constexpr int kAccWave = 64, kAccChunk = RTX_ACC_CHUNK, kAccPitch = 3 * kAccChunk + 1;  // odd pitch: spread LDS banks
 __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const double* __restrict__ L, int64_t npix,
                                                              int K) {
   __shared__ double st[kAccWave * kAccPitch];
@@ -527,7 +533,40 @@ __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const 
   double sum[3] = {0, 0, 0};
   if (t < npx)
     for (int c = 0; c < 3; c++) sum[c] = px.sum[c * npix + p];
+#if RTX_ACC_PIPE
+  // Full chunks with 16-byte-aligned runs (K even) are software-pipelined: chunk i + 1 is
+  // loaded into registers before chunk i is summed out of LDS.  Same adds, same order.
+  constexpr int PP = 3 * kAccChunk / 2;  // 16-byte pieces per pixel run
+  const int kfull = (K & 1) == 0 ? (K / kAccChunk) * kAccChunk : 0;
+  if (kfull > 0) {
+    double2 v[PP];
+    auto load = [&](int k0) {
+#pragma unroll
+      for (int i = 0; i < PP; i++) {
+        const int e = t + kAccWave * i, q = e / PP, j = e - q * PP;
+        if (q < npx) v[i] = *(const double2*)(base + (int64_t)q * 3 * K + 3 * k0 + 2 * j);
+      }
+    };
+    load(0);
+    for (int k0 = 0; k0 < kfull; k0 += kAccChunk) {
+#pragma unroll
+      for (int i = 0; i < PP; i++) {
+        const int e = t + kAccWave * i, q = e / PP, j = e - q * PP;
+        if (q < npx) st[q * kAccPitch + 2 * j] = v[i].x, st[q * kAccPitch + 2 * j + 1] = v[i].y;
+      }
+      __syncthreads();
+      if (k0 + kAccChunk < kfull) load(k0 + kAccChunk);
+      if (t < npx)
+#pragma unroll
+        for (int k = 0; k < kAccChunk; k++)
+          for (int c = 0; c < 3; c++) sum[c] += st[t * kAccPitch + 3 * k + c];
+      __syncthreads();
+    }
+  }
+  for (int k0 = kfull; k0 < K; k0 += kAccChunk) {
+#else
   for (int k0 = 0; k0 < K; k0 += kAccChunk) {
+#endif
     const int kc = std::min(kAccChunk, K - k0);
     if (kc == kAccChunk && (K & 1) == 0) {
       constexpr int PP = 3 * kAccChunk / 2;  // 16-byte pieces per pixel run

@@ -52,6 +52,10 @@ def main():
     ap.add_argument("--mode", default="persistent", choices=["wavefront", "persistent"])
     ap.add_argument("--precision", default="fast", choices=["parity", "fast"])
     ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--schedule", default="auto", choices=["auto", "plain", "park"],
+                    help="persistent fast schedule: auto = timed per scene by the library (default); "
+                         "plain/park force one (identical results; used by scripts/profile.sh so the "
+                         "trace holds no schedule-timing launches)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (=RCCL, one GPU per rank) or gloo (rehearsal)")
@@ -87,6 +91,8 @@ def main():
     p.mode, p.precision = rtx.MODES[args.mode], rtx.PRECISIONS[args.precision]
     if world > 1:
         p.stripe_rows, p.stripe_index, p.stripe_count = STRIPE_ROWS, rank, world
+    sched_flags = {"auto": 0, "park": 2, "plain": 4}[args.schedule]  # RTX_FLAG_PARK / RTX_FLAG_NO_PARK
+    p.flags = sched_flags
     npix = rtx.lib().rtx_render_pixel_count(cam, p)
 
     d_rgb = torch.empty((npix, 3), dtype=torch.float64, device=f"cuda:{dev_id}")
@@ -123,9 +129,9 @@ def main():
         rays_all = float(rays)
 
     # counting pass (diagnostic kernel build) for algorithmic bytes per segment
-    p.flags = 1
+    p.flags = 1 | sched_flags
     cst = step()
-    p.flags = 0
+    p.flags = sched_flags
     segs = max(1, cst["rays_total"])
     nodes_per_seg = cst["node_visits"] / segs
     # SIMD efficiency of the traversal loops (fast BVH4 only): lane work / (64 x wave iterations)

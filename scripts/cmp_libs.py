@@ -22,6 +22,8 @@ CASES = [  # scene recipe, camera preset, width, spp, depth, mode, precision, ad
     ("bunny", "c3_bunny", 96, 8, 20, "persistent", "fast", False),
     ("cornell", "cornell", 64, 16, 50, "persistent", "fast", False),
     ("final", "c2_final", 64, 8, 50, "wavefront", "fast", False),
+    ("final", "c2_final", 48, 100, 50, "persistent", "fast", False),  # many accumulate chunks
+    ("bunny", "c3_bunny", 48, 37, 20, "persistent", "fast", False),  # odd K: unaligned runs
 ]
 
 
