@@ -384,16 +384,56 @@ static int own_sah_node(std::vector<SahItem>& it, int b, int e, std::vector<rtx_
   out[me].is_leaf = 0, out[me].left_first = (uint32_t)l, out[me].right_count = (uint32_t)r;
   return me;
 }
-static void build_own_sah(const rtx_prim* prims, int64_t n, std::vector<rtx_bvh_node>& out) {
-  std::vector<SahItem> it((size_t)n);
+static void build_own_sah(const rtx_prim* prims, int64_t n, const int32_t* skip, int n_skip,
+                          std::vector<rtx_bvh_node>& out) {
+  std::vector<SahItem> it;
+  it.reserve((size_t)n);
   for (int64_t i = 0; i < n; i++) {
-    prim_box(prims[i], it[i].lo, it[i].hi);
-    for (int a = 0; a < 3; a++) it[i].c[a] = 0.5 * (it[i].lo[a] + it[i].hi[a]);
-    it[i].prim = (uint32_t)i;
+    if (std::find(skip, skip + n_skip, (int32_t)i) != skip + n_skip) continue;
+    SahItem x;
+    prim_box(prims[i], x.lo, x.hi);
+    for (int a = 0; a < 3; a++) x.c[a] = 0.5 * (x.lo[a] + x.hi[a]);
+    x.prim = (uint32_t)i;
+    it.push_back(x);
   }
   out.clear();
-  out.reserve(2 * (size_t)n);
-  if (n > 0) own_sah_node(it, 0, (int)n, out);
+  out.reserve(2 * it.size());
+  if (!it.empty()) own_sah_node(it, 0, (int)it.size(), out);
+}
+
+// Primitives the fast path tests outside its tree (DScene::global, trav_globals): up to two
+// whose conservative box has at least the surface area of the union of all other
+// primitives' boxes, i.e. a box that nearly every ray's walk would enter at the root anyway
+// (the ground spheres of the final, bunny and mixed scenes: r = 1000 against a scene a few
+// tens of units wide).  At least two primitives stay in the tree so its root is internal.
+#ifndef RTX_GLOBAL_PRIMS
+#define RTX_GLOBAL_PRIMS 1
+#endif
+static int build_global_prims(const rtx_prim* prims, int64_t n, int32_t out[2]) {
+  int k = 0;
+  if (!RTX_GLOBAL_PRIMS) return 0;
+  while (k < 2 && n - k > 2) {
+    // largest remaining box, and the union of the others
+    int64_t big = -1;
+    double big_area = -1.0;
+    for (int64_t i = 0; i < n; i++) {
+      if (std::find(out, out + k, (int32_t)i) != out + k) continue;
+      double lo[3], hi[3];
+      prim_box(prims[i], lo, hi);
+      const double a = half_area(lo, hi);
+      if (a > big_area) big_area = a, big = i;
+    }
+    double ulo[3] = {INFINITY, INFINITY, INFINITY}, uhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t i = 0; i < n; i++) {
+      if (i == big || std::find(out, out + k, (int32_t)i) != out + k) continue;
+      double lo[3], hi[3];
+      prim_box(prims[i], lo, hi);
+      for (int a = 0; a < 3; a++) ulo[a] = std::min(ulo[a], lo[a]), uhi[a] = std::max(uhi[a], hi[a]);
+    }
+    if (!(big >= 0 && std::isfinite(big_area) && big_area >= half_area(ulo, uhi))) break;
+    out[k++] = (int32_t)big;
+  }
+  return k;
 }
 
 int pick_stack(int depth) {
@@ -623,6 +663,8 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   sc->n_nodes = d->nodes ? d->n_nodes : 0;
   std::vector<FNode> fn;
   std::vector<F4Node> f4;
+  int32_t global[2] = {0, 0};
+  int n_global = 0;
   if (d->nodes && d->n_nodes > 0) {
     if ((rc = upload(sc->nodes, d->nodes, d->n_nodes, s))) return rc;
     const int depth = bvh_depth(d->nodes, d->n_nodes);
@@ -633,7 +675,8 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
 #if RTX_BVH4
 #if RTX_FAST_TREE
       std::vector<rtx_bvh_node> own;
-      build_own_sah(d->prims, d->n_prims, own);
+      n_global = build_global_prims(d->prims, d->n_prims, global);
+      build_own_sah(d->prims, d->n_prims, global, n_global, own);
       const int need = build_fast4(own.data(), d->prims, f4);
 #else
       const int need = build_fast4(d->nodes, d->prims, f4);
@@ -660,6 +703,8 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   S.n_prims = S.use_bvh ? d->n_prims : d->n_prims;
   S.froot_leaf = 0, S.froot_count = 0;
   S.has_tris = 0;
+  S.n_global = sc->fast_ok ? n_global : 0;
+  S.global[0] = global[0], S.global[1] = global[1];
   for (int64_t i = 0; i < d->n_prims && !S.has_tris; i++) S.has_tris = d->prims[i].kind == RTX_PRIM_TRIANGLE;
   if (S.use_bvh && d->nodes[0].is_leaf) S.froot_leaf = 1, S.froot_count = (int32_t)d->nodes[0].right_count;
   if (!d->nodes && d->n_nodes == 0) S.use_bvh = 0;

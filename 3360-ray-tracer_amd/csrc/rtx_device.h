@@ -221,6 +221,8 @@ struct DScene {
   int32_t froot_leaf;  // fast BVH: the whole tree is one leaf (count in froot_count)
   int32_t froot_count;
   int32_t has_tris;  // any triangle: prim_t preloads all 80 record bytes, else the first 48
+  int32_t n_global;   // fast BVH: primitives kept out of the tree, tested before every walk
+  int32_t global[2];  // their indices into prims (see build_global_prims, rtx_capi.hip)
 };
 
 struct Hit {  // HitRecord (hittable.h:18-42)
@@ -801,6 +803,11 @@ __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, doub
     t_best = closest;
     return best;
   }
+  for (int i = 0; i < S.n_global; i++) {
+    const int64_t gi = S.global[i];
+    if (COUNT) count_prim(cnt, S.prims + gi);
+    if (prim_t(S.prims + gi, S.has_tris, o, d, tmin, closest, t, m)) closest = t, best = gi, mat_best = m;
+  }
   const FRay4 r = make_fray4(o, d);
   float tmax_f = f32_round_up(closest);
   int sp = 0;
@@ -943,6 +950,27 @@ __device__ __forceinline__ void trav_init(TravState& ts, double tmax) {
   ts.tmax_f = f32_round_up(tmax);
 }
 
+// Primitives kept out of the fast tree (a box as large as the rest of the scene together,
+// e.g. a ground sphere; build_global_prims) are tested by every ray right after trav_init, in
+// the converged control flow of the walk's start, instead of at scattered node visits where a
+// few lanes at a time would run them.  Testing a primitive earlier only tightens `closest`
+// sooner, so the closest hit is unchanged (up to the order of exact t ties, as for any tree).
+template <bool COUNT>
+__device__ __forceinline__ void trav_globals(const DScene& S, V3 o, V3 d, double tmin, Counters& cnt, TravState& ts) {
+  for (int i = 0; i < S.n_global; i++) {
+    const uint32_t gi = (uint32_t)S.global[i];
+    if (COUNT) {
+      count_prim(cnt, S.prims + gi);
+      if (first_active_lane()) cnt.wprims++;
+    }
+    double t;
+    int32_t m;
+    if (prim_t(S.prims + gi, S.has_tris, o, d, tmin, ts.closest, t, m))
+      ts.closest = t, ts.best = (int32_t)gi, ts.mat = m;
+  }
+  if (S.n_global) ts.tmax_f = f32_round_up(ts.closest);
+}
+
 template <int STACK, bool COUNT>
 __device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double tmin, uint32_t* stk, int stride,
                                            Counters& cnt, TravState& ts, int park_at) {
@@ -1056,6 +1084,7 @@ __device__ __forceinline__ int64_t trace_fast4_lean(const DScene& S, V3 o, V3 d,
   if (!S.use_bvh || S.froot_leaf) return trace_flat(S, o, d, tmin, tmax, cnt, COUNT, t_best, mat_best);
   TravState ts;
   trav_init(ts, tmax);
+  trav_globals<COUNT>(S, o, d, tmin, cnt, ts);
   trace4_run<STACK, COUNT>(S, o, d, tmin, stk, stride, cnt, ts, -1);
   t_best = ts.closest, mat_best = ts.mat;
   return ts.best;

@@ -398,7 +398,10 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
       int64_t best;
       if (kPark && park_ok) {
         const int active = __popcll(__ballot(1));  // lanes tracing this round
-        if (!parked) trav_init(trs, kInf);
+        if (!parked) {
+          trav_init(trs, kInf);
+          trav_globals<COUNT>(A.S, P.o, P.d, tmin, c, trs);
+        }
         // parking only when some lane of this round finishes first: every round makes progress
         const bool done = trace4_run<STACK, COUNT>(A.S, P.o, P.d, tmin, stk, kBlock, c, trs,
                                                    active > RTX_PARK ? RTX_PARK : -1);
