@@ -75,6 +75,36 @@ def test_intersect_fast_matches_parity(dev_scenes, scene):
     assert same.mean() >= 0.9995, np.nonzero(~same)[0][:5]
 
 
+@pytest.mark.parametrize("n_small", [3, 12])
+def test_global_primitives_split(rtx_mod, tmp_path, n_small):
+    """Ground-sized primitives are kept out of the fast tree and tested before every walk
+    (build_global_prims / trav_globals): the fast closest hits still equal the parity ones.
+    Two huge spheres qualify here: the ground and a sphere nested inside it, which rays that
+    start inside the ground (y < 0) reach."""
+    rng = np.random.default_rng(11 + n_small)
+    lines = ["rtxscene 1", "bvh 1", "tex 0 solid 0.5 0.5 0.5", "mat 0 lambertian 0",
+             "sphere 0 -1000 0 1000 0", "sphere 0 -1000 0 950 0"]
+    for i in range(n_small):
+        c = rng.uniform(-4, 4, 3)
+        c[1] = abs(c[1]) * 0.5
+        lines.append("sphere %r %r %r %r 0" % (float(c[0]), float(c[1]), float(c[2]), float(rng.uniform(0.2, 1.0))))
+    lines.append("sphere 0 0.5 0 0.5 0")  # resting on the ground: t-close to it near the contact
+    p = tmp_path / "globals.rtxs"
+    p.write_text("\n".join(lines) + "\n")
+    d = rtx_mod.DeviceScene(rtx_mod.HostScene.load(str(p)))
+    n = 40_000
+    o = np.column_stack([rng.uniform(-8, 8, n), rng.uniform(0.1, 6, n), rng.uniform(6, 14, n)])
+    o[::4, 1] = -20.0  # inside the ground, above the nested sphere
+    t = np.column_stack([rng.uniform(-6, 6, n), rng.uniform(-3, 3, n), rng.uniform(-6, 6, n)])
+    rays = np.hstack([o, t - o])
+    a = hit_matrix(d.intersect(rays, precision="parity"))
+    b = hit_matrix(d.intersect(rays, precision="fast"))
+    cols = [0, 1, 2, 3, 4, 5, 6, 7, 10, 11]
+    same = np.all(a[:, cols] == b[:, cols], 1)
+    assert a[:, 0].mean() > 0.5
+    assert same.all(), np.nonzero(~same)[0][:5]
+
+
 def test_intersect_large_batch_and_tmax(dev_scenes, rtx_mod):
     d = dev_scenes("bunny")
     rng = np.random.default_rng(1)
