@@ -488,7 +488,7 @@ int launch_intersect(rtx_scene* sc, const rtx_ray* d_rays, int64_t n, rtx_hit* d
                      hipStream_t s) {
   const int64_t blocks = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL((k_intersect<STACK, FAST>), dim3((unsigned)blocks), dim3(kBlock),
-                     STACK * kBlock * sizeof(uint32_t), s, sc->S, d_rays, n, d_hits, tmin, tmax);
+                     stack_lds_bytes(STACK), s, sc->S, d_rays, n, d_hits, tmin, tmax);
   HIPC(hipGetLastError());
   return RTX_OK;
 }
@@ -510,7 +510,7 @@ struct Launch {
 
 template <int STACK, bool FAST, bool COUNT>
 int run_extend(const Launch& L, const RenderArgs& A, const PathQueue& q, const unsigned* cnt, int64_t max_items) {
-  const size_t lds = STACK * kBlock * sizeof(uint32_t);
+  const size_t lds = stack_lds_bytes(STACK);
   const int64_t need = (max_items + kBlock - 1) / kBlock;
   const int grid = (int)std::max<int64_t>(
       1, std::min<int64_t>(need, persistent_grid(L.sc, (const void*)k_wf_extend<STACK, FAST, COUNT>, lds)));
@@ -521,7 +521,7 @@ int run_extend(const Launch& L, const RenderArgs& A, const PathQueue& q, const u
 
 template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK>
 int run_persistent(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
-  const size_t lds = STACK * kBlock * sizeof(uint32_t);
+  const size_t lds = stack_lds_bytes(STACK);
   const int grid = persistent_grid(L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK>, lds);
   hipLaunchKernelGGL((k_persistent<STACK, FAST, COUNT, SCATTER, PARK>), dim3(grid), dim3(kBlock), lds, L.s, A,
                      next_slot);

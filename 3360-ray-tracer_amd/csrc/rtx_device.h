@@ -910,6 +910,9 @@ __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, doub
 // inside s = 1e-5, and < 2^-23 |n0| absolute, inside the outward offset delta = 2^-20 |n0|
 // (see FRay4), so the test stays conservative.  Node loads use a 32-bit byte offset from the
 // (uniform) node-array base.
+#ifndef RTX_PUSH_BRANCHLESS
+#define RTX_PUSH_BRANCHLESS 1  // lean walk: unconditional child stores, sp advanced per entered child
+#endif
 struct FRay4L {
   float iex, iey, iez, nex, ney, nez;  // entry planes: inverse and offset, scaled by (1 - s)
   float ixx, ixy, ixz, nxx, nxy, nxz;  // exit planes: scaled by (1 + s)
@@ -1043,6 +1046,19 @@ __device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double t
     cswap4(tt[1], cc[1], tt[3], cc[3]);
     cswap4(tt[1], cc[1], tt[2], cc[2]);
     if (tt[0] != __builtin_inff()) {
+#if RTX_PUSH_BRANCHLESS
+      // The sort leaves the entered children as a prefix (the others carry +inf and sort
+      // last), so the pushes are unconditional stores at sp, with sp advanced only for an
+      // entered child: the store of a child not entered is overwritten by the next one or
+      // lies just above the stack top.  build_fast4 bounds sp by the tree's exact worst case
+      // (need <= STACK, checked on the host), so every store index is <= STACK and the
+      // kernels give each lane STACK + 1 slots (stack_lds_bytes).
+#pragma unroll
+      for (int c = 3; c >= 1; c--) {
+        stk[sp * stride] = (uint32_t)cc[c];
+        sp += tt[c] != __builtin_inff() ? 1 : 0;
+      }
+#else
 #pragma unroll
       for (int c = 3; c >= 1; c--) {
         if (tt[c] != __builtin_inff()) {
@@ -1050,6 +1066,7 @@ __device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double t
           stk[(sp++) * stride] = (uint32_t)cc[c];
         }
       }
+#endif
       node = (uint32_t)cc[0];
     } else {
       if (sp == 0) break;

@@ -115,6 +115,10 @@ __device__ __forceinline__ int64_t wave_compact(bool want, unsigned int* counter
 // mat_best: the closest primitive's material id (or -1); the fast traversal keeps it from the
 // primitive record it already loaded, so shading can fetch the material without first
 // waiting for the record.
+// LDS of a block's traversal stacks: STACK + 1 slots per lane (the branchless pushes of the
+// lean walk may store one slot above the deepest entry, see trace4_run).
+constexpr size_t stack_lds_bytes(int STACK) { return (size_t)(STACK + 1) * kBlock * sizeof(uint32_t); }
+
 template <int STACK, bool FAST, bool COUNT>
 __device__ __forceinline__ int64_t trace(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
                                          Counters& c, double& t_best, int32_t& mat_best) {
