@@ -620,7 +620,16 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   for (auto& e : sc->ev) HIPC(hipEventCreate(&e));
   hipStream_t s = sc->stream;
   int rc;
-  if ((rc = upload(sc->prims, d->prims, d->n_prims, s))) return rc;
+  if (RTX_TRI_EDGES) {  // device table: triangles carry A, B - A, C - A (tri_e1 / tri_e2)
+    std::vector<rtx_prim> dp(d->prims, d->prims + d->n_prims);
+    for (rtx_prim& q : dp)
+      if (q.kind == RTX_PRIM_TRIANGLE)
+        for (int a = 0; a < 3; a++) q.g[3 + a] = q.g[3 + a] - q.g[a], q.g[6 + a] = q.g[6 + a] - q.g[a];
+    if ((rc = upload(sc->prims, dp.data(), dp.size(), s))) return rc;
+    HIPC(hipStreamSynchronize(s));  // dp is a temporary: the copy must finish before it goes
+  } else if ((rc = upload(sc->prims, d->prims, d->n_prims, s))) {
+    return rc;
+  }
   // Device copy of the material table: a Lambertian / DiffuseLight whose texture is a
   // SolidColor carries the colour itself (texture = -1, colour in the unused albedo field),
   // so shading skips the dependent texture-table load (mat_tex, rtx_device.h).

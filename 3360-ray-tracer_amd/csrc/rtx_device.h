@@ -275,11 +275,26 @@ __device__ __forceinline__ bool hit_sphere(const double* g, int32_t mat, V3 o, V
   return true;
 }
 
+// Triangle edges e1 = B - A, e2 = C - A (triangle.h:45-46).  With RTX_TRI_EDGES the device
+// copy of the primitive table stores them in place of B and C (rtx_scene_create computes the
+// same IEEE double differences on the host), so the tests read them instead of subtracting.
+#ifndef RTX_TRI_EDGES
+#define RTX_TRI_EDGES 1
+#endif
+__device__ __forceinline__ V3 tri_e1(const double* g) {
+  if (RTX_TRI_EDGES) return V3{g[3], g[4], g[5]};
+  return V3{g[3], g[4], g[5]} - V3{g[0], g[1], g[2]};
+}
+__device__ __forceinline__ V3 tri_e2(const double* g) {
+  if (RTX_TRI_EDGES) return V3{g[6], g[7], g[8]};
+  return V3{g[6], g[7], g[8]} - V3{g[0], g[1], g[2]};
+}
+
 // Triangle::Hit (triangle.h:41-87): f32 det/inv_det/u/v/t, inclusive range, u,v untouched.
 __device__ __forceinline__ bool hit_triangle(const double* g, int32_t mat, V3 o, V3 d, double tmin, double tmax,
                                              Hit& rec) {
-  V3 A{g[0], g[1], g[2]}, B{g[3], g[4], g[5]}, C{g[6], g[7], g[8]};
-  V3 e1 = B - A, e2 = C - A;
+  V3 A{g[0], g[1], g[2]};
+  V3 e1 = tri_e1(g), e2 = tri_e2(g);
   V3 pvec = cross(d, e2);
   float det = (float)dot(e1, pvec);
   if (fabsf(det) < 1e-6f) return false;
@@ -388,8 +403,8 @@ __device__ __forceinline__ bool prim_t(const rtx_prim* __restrict__ Pp, bool tri
   const PrimRec* P = &R;
   const int kind = P->kind;
   if (kind == RTX_PRIM_TRIANGLE) {
-    V3 A{P->g[0], P->g[1], P->g[2]}, B{P->g[3], P->g[4], P->g[5]}, C{P->g[6], P->g[7], P->g[8]};
-    V3 e1 = B - A, e2 = C - A;
+    V3 A{P->g[0], P->g[1], P->g[2]};
+    V3 e1 = tri_e1(P->g), e2 = tri_e2(P->g);
     V3 pvec = cross(d, e2);
     float det = (float)dot(e1, pvec);
     if (fabsf(det) < 1e-6f) return false;
@@ -471,8 +486,7 @@ __device__ __forceinline__ void finish_hit_at(const DScene& S, int64_t best, dou
     if (UV) sphere_uv(outward, h.u, h.v);
     else h.lazy_sphere = best;
   } else if (kind == RTX_PRIM_TRIANGLE) {  // hit_triangle after t
-    const V3 A{P->g[0], P->g[1], P->g[2]}, B{P->g[3], P->g[4], P->g[5]}, C{P->g[6], P->g[7], P->g[8]};
-    const V3 e1 = B - A, e2 = C - A;
+    const V3 e1 = tri_e1(P->g), e2 = tri_e2(P->g);
     h.p = o + h.t * d;
     set_face_normal(h, d, normalize(cross(e1, e2)));
   } else {  // hit_rect after t
