@@ -198,6 +198,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_intersect(DScene S,
 // ---------------------------------------------------------------------------------------
 // Wavefront: primary generation for every slot of active pixels
 // ---------------------------------------------------------------------------------------
+#ifndef RTX_PERSISTENT_ONLY  // rtx_park.hip: the persistent kernel's PARK instantiations only
 __global__ __launch_bounds__(kBlock) void k_wf_generate(RenderArgs A, PathQueue q, unsigned int* count) {
   const int64_t nslots = A.npix * A.K;
   uint32_t made = 0;
@@ -226,6 +227,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_generate(RenderArgs A, PathQueue 
   }
   flush_counters(A, Counters{0, 0, 0, 0, 0, 0}, 0, made, false);
 }
+#endif
 
 // Closest hit for every queued path (one ray per lane, grid-stride).
 template <int STACK, bool FAST, bool COUNT>
@@ -247,6 +249,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_wf_extend(RenderArg
 }
 
 // Shading for every queued path + compacted child queue (wavefront.cc:109-217).
+#ifndef RTX_PERSISTENT_ONLY  // rtx_park.hip: the persistent kernel's PARK instantiations only
 __global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in, const unsigned int* in_count,
                                                      PathQueue out, unsigned int* out_count) {
   const int64_t n = *in_count;
@@ -286,6 +289,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in,
     }
   }
 }
+#endif
 
 // ---------------------------------------------------------------------------------------
 // Persistent lanes: each lane owns one path at a time and refills from a global slot
@@ -469,6 +473,22 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
   flush_counters(A, c, segs, prims, COUNT);
 }
 
+// The PARK instantiations are compiled in their own translation unit (rtx_park.hip) with the
+// LLVM max-memory-clause scheduler, which suits their latency-bound walk (bunny +1.5 %,
+// `ab_sched2_*`) but not the plain kernel.  Scheduling only: the same arithmetic.
+#ifndef RTX_PARK_TU
+#define RTX_PARK_TU 1
+#endif
+#define RTX_PARK_INSTANCES(X) \
+  X(32, false, false) X(32, true, false) X(64, false, false) X(64, true, false) \
+  X(32, false, true) X(32, true, true) X(64, false, true) X(64, true, true)
+#if RTX_PARK_TU && !defined(RTX_PERSISTENT_ONLY)
+#define RTX_PARK_EXTERN(ST, CO, SC) \
+  extern template __global__ void k_persistent<ST, true, CO, SC, true>(RenderArgs, unsigned long long*);
+RTX_PARK_INSTANCES(RTX_PARK_EXTERN)
+#undef RTX_PARK_EXTERN
+#endif
+
 // ---------------------------------------------------------------------------------------
 // RecordSample in sample order (pixel_state.h:22-39) + IsConverged (pixel_state.h:54-72)
 // ---------------------------------------------------------------------------------------
@@ -478,6 +498,7 @@ struct PixelSoA {
   uint8_t* conv;
 };
 
+#ifndef RTX_PERSISTENT_ONLY  // rtx_park.hip: the persistent kernel's PARK instantiations only
 __global__ __launch_bounds__(kBlock) void k_accumulate(PixelSoA px, const double* __restrict__ L, int64_t npix,
                                                        int K, int adaptive, int min_spp, double rel) {
   const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -515,6 +536,7 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(PixelSoA px, const double
   px.samples[p] = n;
   px.conv[p] = conv;
 }
+#endif
 
 // Fixed-spp accumulation: the sum RecordSample (and DefaultSampler) forms, in sample order.
 // One wave per 64 consecutive pixels, whose radiance runs are one contiguous region of Lbuf
@@ -529,6 +551,7 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(PixelSoA px, const double
 #define RTX_ACC_PIPE 1  // accumulate: the next chunk's loads are in flight while the current one is summed
 #endif
 constexpr int kAccWave = 64, kAccChunk = RTX_ACC_CHUNK, kAccPitch = 3 * kAccChunk + 1;  // odd pitch: spread LDS banks
+#ifndef RTX_PERSISTENT_ONLY  // rtx_park.hip: the persistent kernel's PARK instantiations only
 __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const double* __restrict__ L, int64_t npix,
                                                              int K) {
   __shared__ double st[kAccWave * kAccPitch];
@@ -606,6 +629,7 @@ __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const 
     px.samples[p] += K;
   }
 }
+#endif
 
 // AdaptiveSampler::SamplePixel (sampler.h:44-82) replayed in sample order for the MegaKernel
 // renderer.  Its quirks are kept: `pixel` is the running SUM of the samples and the mean /
@@ -615,6 +639,7 @@ __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const 
 __device__ __forceinline__ double luminance(double x, double y, double z) {
   return (double)0.2126f * x + (double)0.7152f * y + (double)0.0722f * z;
 }
+#ifndef RTX_PERSISTENT_ONLY  // rtx_park.hip: the persistent kernel's PARK instantiations only
 __global__ __launch_bounds__(kBlock) void k_accumulate_mk_adaptive(PixelSoA px, const double* __restrict__ L,
                                                                    int64_t npix, int K, int min_samples,
                                                                    int max_samples, double threshold) {
@@ -652,10 +677,12 @@ __global__ __launch_bounds__(kBlock) void k_accumulate_mk_adaptive(PixelSoA px, 
   px.samples[p] = n;
   px.conv[p] = done ? 1 : 0;
 }
+#endif
 
 // wavefront.cc:229-235: sum / (float)samples  (Vec3 operator/ is (1/t)*v); megakernel
 // (mega_kernel.h + sampler.h:32,79): pixel /= num_samples (DefaultSampler) or /= samples
 // (AdaptiveSampler).
+#ifndef RTX_PERSISTENT_ONLY  // rtx_park.hip: the persistent kernel's PARK instantiations only
 __global__ __launch_bounds__(kBlock) void k_resolve(PixelSoA px, int64_t npix, int megakernel, int spp,
                                                     double* __restrict__ rgb, int32_t* __restrict__ spp_out) {
   // megakernel: 1 = DefaultSampler (divide by spp), 2 = AdaptiveSampler (by the pixel's count)
@@ -669,5 +696,6 @@ __global__ __launch_bounds__(kBlock) void k_resolve(PixelSoA px, int64_t npix, i
   for (int c = 0; c < 3; c++) rgb[3 * p + c] = (megakernel || n > 0) ? s * px.sum[c * npix + p] : 0.0;
   if (spp_out) spp_out[p] = megakernel == 1 ? spp : n;
 }
+#endif
 
 }  // namespace rtxd

@@ -1,0 +1,17 @@
+// PARK instantiations of the persistent kernel (k_persistent<STACK, true, COUNT, SCATTER,
+// true>), compiled apart from rtx_capi.hip so this translation unit can use the LLVM
+// max-memory-clause scheduler (see the Makefile and rtx_kernels.h).
+#define RTX_PERSISTENT_ONLY 1
+#include <hip/hip_runtime.h>
+
+#include "rtx.h"
+#include "rtx_kernels.h"
+
+#if RTX_PARK_TU  // else rtx_capi.hip instantiates them itself
+namespace rtxd {
+#define RTX_PARK_DEFINE(ST, CO, SC) \
+  template __global__ void k_persistent<ST, true, CO, SC, true>(RenderArgs, unsigned long long*);
+RTX_PARK_INSTANCES(RTX_PARK_DEFINE)
+#undef RTX_PARK_DEFINE
+}  // namespace rtxd
+#endif
