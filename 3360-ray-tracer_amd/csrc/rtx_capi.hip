@@ -906,7 +906,8 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
     q.hit = (int32_t*)(q.meta + nslots);
     return q;
   };
-  // per-launch timing of the dominant kernel (extend / persistent) with an event pool
+  // per-launch timing of the dominant kernel (extend / persistent) with an event pool: one
+  // pair per hot launch of the whole frame (grow-only pool)
   size_t evi = 0;
   auto ev_at = [&](size_t i) -> hipEvent_t {
     while (sc->evpool.size() <= i) {
@@ -930,7 +931,6 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
       Kc = std::min(Kc, s0 < prm->min_spp ? prm->min_spp - s0 : 4);
     A.K = Kc;
     A.s0 = s0;
-    evi = 0;
     auto hot_begin = [&]() -> int {
       if (timed) {
         hipEvent_t e = ev_at(evi++);
@@ -963,14 +963,6 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
       if ((rc = hot_begin())) return rc;
       hot_launches++;
     }
-    if (timed) {
-      HIPC(hipEventSynchronize(sc->evpool[evi - 1]));
-      for (size_t e = 0; e + 1 < evi; e += 2) {
-        float ms = 0;
-        HIPC(hipEventElapsedTime(&ms, sc->evpool[e], sc->evpool[e + 1]));
-        hot_ms += ms;
-      }
-    }
     if (mk_adaptive)
       hipLaunchKernelGGL(k_accumulate_mk_adaptive, dim3(pix_blocks), dim3(kBlock), 0, s, px, A.L, npix, Kc,
                          prm->min_spp, prm->spp, prm->rel_threshold);
@@ -993,6 +985,13 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
     HIPC(hipEventSynchronize(sc->ev[1]));
     float ms = 0;
     HIPC(hipEventElapsedTime(&ms, sc->ev[0], sc->ev[1]));
+    // the hot launches' event pairs are read only now: no host wait inside the frame, so the
+    // accumulate / resolve launches are queued while the hot kernel still runs
+    for (size_t e = 0; e + 1 < evi; e += 2) {
+      float hms = 0;
+      HIPC(hipEventElapsedTime(&hms, sc->evpool[e], sc->evpool[e + 1]));
+      hot_ms += hms;
+    }
     unsigned long long h[8];
     HIPC(hipMemcpy(h, cnt, sizeof h, hipMemcpyDeviceToHost));
     stats->rays_total = h[0];
