@@ -40,7 +40,10 @@ constexpr int kBlock = 256;
 #define RTX_EARLY_MAT 0  // persistent: material fetched by the id the traversal kept, beside the record (A/B r01: -2% C2, +-0 bunny)
 #endif
 #ifndef RTX_REFILL_MIN
-#define RTX_REFILL_MIN 32  // persistent lanes: refill once this many lanes of a wave are idle (A/B: 1/8/16/32)
+#define RTX_REFILL_MIN 24  // persistent lanes: refill once this many lanes of a wave are idle (A/B: ab_refill2_*)
+#endif
+#ifndef RTX_REFILL_MIN_PARK
+#define RTX_REFILL_MIN_PARK 16  // the same for the PARK kernel
 #endif
 
 // Pixel subset of the image handled by one call (rectangle or interleaved row stripes).
@@ -347,7 +350,8 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
     // primary-generation code over several lanes.
     const unsigned long long idle = __ballot(!has);
     bool fresh = false;
-    if (idle != 0 && !exhausted && (__popcll(idle) >= RTX_REFILL_MIN || idle == ~0ull)) {
+    constexpr int kRefillMin = kPark ? RTX_REFILL_MIN_PARK : RTX_REFILL_MIN;
+    if (idle != 0 && !exhausted && (__popcll(idle) >= kRefillMin || idle == ~0ull)) {
       const uint64_t nidle = (uint64_t)__popcll(idle);
       const uint64_t rank = (uint64_t)__popcll(idle & ((1ull << lane_id()) - 1ull));
       uint64_t cand = ~0ull;
