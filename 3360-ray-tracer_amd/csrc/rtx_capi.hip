@@ -519,14 +519,21 @@ int run_extend(const Launch& L, const RenderArgs& A, const PathQueue& q, const u
   return RTX_OK;
 }
 
-template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK>
-int run_persistent(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
+template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK>
+int run_persistent_k(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
   const size_t lds = stack_lds_bytes(STACK);
-  const int grid = persistent_grid(L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK>, lds);
-  hipLaunchKernelGGL((k_persistent<STACK, FAST, COUNT, SCATTER, PARK>), dim3(grid), dim3(kBlock), lds, L.s, A,
+  const int grid = persistent_grid(L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK>, lds);
+  hipLaunchKernelGGL((k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK>), dim3(grid), dim3(kBlock), lds, L.s, A,
                      next_slot);
   HIPC(hipGetLastError());
   return RTX_OK;
+}
+// PARK frames of a scene whose fast tree holds triangles only run the triangle-only build
+template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK>
+int run_persistent(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
+  constexpr int TK = (FAST && !COUNT && !SCATTER && PARK && RTX_TREE_KIND) ? (int)RTX_PRIM_TRIANGLE : -1;
+  if (TK >= 0 && A.S.tree_kind == TK) return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK>(L, A, next_slot);
+  return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, -1>(L, A, next_slot);
 }
 
 // template dispatch helpers
@@ -713,6 +720,15 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   S.froot_leaf = 0, S.froot_count = 0;
   S.has_tris = 0;
   S.n_global = sc->fast_ok ? n_global : 0;
+  S.tree_kind = -1;
+  if (sc->fast_ok && d->n_prims > 0) {  // the one kind of the tree's primitives (globals excluded)
+    int k = -2;
+    for (int64_t i = 0; i < d->n_prims && k != -1; i++) {
+      if ((n_global > 0 && global[0] == i) || (n_global > 1 && global[1] == i)) continue;
+      k = k == -2 ? d->prims[i].kind : (k == d->prims[i].kind ? k : -1);
+    }
+    S.tree_kind = k < 0 ? -1 : k;
+  }
   S.global[0] = global[0], S.global[1] = global[1];
   for (int64_t i = 0; i < d->n_prims && !S.has_tris; i++) S.has_tris = d->prims[i].kind == RTX_PRIM_TRIANGLE;
   if (S.use_bvh && d->nodes[0].is_leaf) S.froot_leaf = 1, S.froot_count = (int32_t)d->nodes[0].right_count;

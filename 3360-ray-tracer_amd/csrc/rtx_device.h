@@ -221,6 +221,7 @@ struct DScene {
   int32_t froot_leaf;  // fast BVH: the whole tree is one leaf (count in froot_count)
   int32_t froot_count;
   int32_t has_tris;  // any triangle: prim_t preloads all 80 record bytes, else the first 48
+  int32_t tree_kind;  // fast BVH: the one kind of every primitive in the tree, or -1
   int32_t n_global;   // fast BVH: primitives kept out of the tree, tested before every walk
   int32_t global[2];  // their indices into prims (see build_global_prims, rtx_capi.hip)
 };
@@ -396,12 +397,15 @@ __device__ __forceinline__ PrimRec load_prim(const rtx_prim* __restrict__ P, boo
   return r;
 }
 
+// KIND >= 0: every primitive this call can see has that kind (DScene::tree_kind), so the
+// other kinds' branches are compiled out.
+template <int KIND = -1>
 __device__ __forceinline__ bool prim_t(const rtx_prim* __restrict__ Pp, bool tris, V3 o, V3 d, double tmin,
                                        double tmax, double& t_out, int32_t& mat_out) {
-  const PrimRec R = load_prim(Pp, tris);
+  const PrimRec R = load_prim(Pp, KIND < 0 ? tris : KIND == (int)RTX_PRIM_TRIANGLE);
   mat_out = R.mat;
   const PrimRec* P = &R;
-  const int kind = P->kind;
+  const int kind = KIND >= 0 ? KIND : P->kind;
   if (kind == RTX_PRIM_TRIANGLE) {
     V3 A{P->g[0], P->g[1], P->g[2]};
     V3 e1 = tri_e1(P->g), e2 = tri_e2(P->g);
@@ -988,7 +992,7 @@ __device__ __forceinline__ void trav_globals(const DScene& S, V3 o, V3 d, double
   if (S.n_global) ts.tmax_f = f32_round_up(ts.closest);
 }
 
-template <int STACK, bool COUNT>
+template <int STACK, bool COUNT, int KIND = -1>
 __device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double tmin, uint32_t* stk, int stride,
                                            Counters& cnt, TravState& ts, int park_at) {
   const FRay4L r = make_fray4l(o, d);
@@ -1043,7 +1047,7 @@ __device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double t
           count_prim(cnt, S.prims + cur);
           if (first_active_lane()) cnt.wprims++;
         }
-        if (prim_t(S.prims + cur, S.has_tris, o, d, tmin, closest, t, m))
+        if (prim_t<KIND>(S.prims + cur, S.has_tris, o, d, tmin, closest, t, m))
           closest = t, best = (int32_t)cur, mat_best = m, shrink = true;
       }
       if (shrink) {

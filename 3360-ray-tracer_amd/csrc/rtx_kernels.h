@@ -308,7 +308,10 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in,
 #endif
 constexpr int kChunk = RTX_CHUNK;
 
-template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK>
+// TK >= 0 (PARK schedule only): every primitive in the fast tree has kind TK (the bunny: the
+// ground sphere is a global primitive, the tree holds triangles), so the walk's leaf tests
+// are compiled for that kind alone.
+template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK = -1>
 __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderArgs A, unsigned long long* next_slot) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* stk = lds + threadIdx.x;
@@ -415,7 +418,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
           trav_globals<COUNT>(A.S, P.o, P.d, tmin, c, trs);
         }
         // parking only when some lane of this round finishes first: every round makes progress
-        const bool done = trace4_run<STACK, COUNT>(A.S, P.o, P.d, tmin, stk, kBlock, c, trs,
+        const bool done = trace4_run<STACK, COUNT, TK>(A.S, P.o, P.d, tmin, stk, kBlock, c, trs,
                                                    active > RTX_PARK ? RTX_PARK : -1);
         parked = !done;
         if (parked) continue;
@@ -486,11 +489,20 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
 #define RTX_PARK_INSTANCES(X) \
   X(32, false, false) X(32, true, false) X(64, false, false) X(64, true, false) \
   X(32, false, true) X(32, true, true) X(64, false, true) X(64, true, true)
+#ifndef RTX_TREE_KIND
+#define RTX_TREE_KIND 1  // PARK kernel specialised for triangle-only trees
+#endif
+#define RTX_PARK_TRI_INSTANCES(Y) Y(32) Y(64)
 #if RTX_PARK_TU && !defined(RTX_PERSISTENT_ONLY)
 #define RTX_PARK_EXTERN(ST, CO, SC) \
   extern template __global__ void k_persistent<ST, true, CO, SC, true>(RenderArgs, unsigned long long*);
 RTX_PARK_INSTANCES(RTX_PARK_EXTERN)
 #undef RTX_PARK_EXTERN
+#define RTX_PARK_TRI_EXTERN(ST) \
+  extern template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE>(RenderArgs, \
+                                                                                              unsigned long long*);
+RTX_PARK_TRI_INSTANCES(RTX_PARK_TRI_EXTERN)
+#undef RTX_PARK_TRI_EXTERN
 #endif
 
 // ---------------------------------------------------------------------------------------
