@@ -528,10 +528,12 @@ int run_persistent_k(const Launch& L, const RenderArgs& A, unsigned long long* n
   HIPC(hipGetLastError());
   return RTX_OK;
 }
-// PARK frames of a scene whose fast tree holds triangles only run the triangle-only build
+// fast frames of a scene whose tree holds one kind run a build for that kind: triangles with
+// the PARK schedule (the bunny), spheres with the plain one (the final and mixed scenes)
 template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK>
 int run_persistent(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
-  constexpr int TK = (FAST && !COUNT && !SCATTER && PARK && RTX_TREE_KIND) ? (int)RTX_PRIM_TRIANGLE : -1;
+  constexpr bool spec = FAST && !COUNT && !SCATTER && RTX_TREE_KIND;
+  constexpr int TK = spec ? (PARK ? (int)RTX_PRIM_TRIANGLE : (int)RTX_PRIM_SPHERE) : -1;
   if (TK >= 0 && A.S.tree_kind == TK) return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK>(L, A, next_slot);
   return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, -1>(L, A, next_slot);
 }

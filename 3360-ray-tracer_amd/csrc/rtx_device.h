@@ -1112,7 +1112,7 @@ __device__ __forceinline__ int64_t trace_flat(const DScene& S, V3 o, V3 d, doubl
   return best;
 }
 
-template <int STACK, bool COUNT>
+template <int STACK, bool COUNT, int KIND = -1>
 __device__ __forceinline__ int64_t trace_fast4_lean(const DScene& S, V3 o, V3 d, double tmin, double tmax,
                                                     uint32_t* stk, int stride, Counters& cnt, double& t_best,
                                                     int32_t& mat_best) {
@@ -1120,7 +1120,7 @@ __device__ __forceinline__ int64_t trace_fast4_lean(const DScene& S, V3 o, V3 d,
   TravState ts;
   trav_init(ts, tmax);
   trav_globals<COUNT>(S, o, d, tmin, cnt, ts);
-  trace4_run<STACK, COUNT>(S, o, d, tmin, stk, stride, cnt, ts, -1);
+  trace4_run<STACK, COUNT, KIND>(S, o, d, tmin, stk, stride, cnt, ts, -1);
   t_best = ts.closest, mat_best = ts.mat;
   return ts.best;
 }

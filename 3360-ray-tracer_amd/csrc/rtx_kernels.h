@@ -122,12 +122,12 @@ __device__ __forceinline__ int64_t wave_compact(bool want, unsigned int* counter
 // lean walk may store one slot above the deepest entry, see trace4_run).
 constexpr size_t stack_lds_bytes(int STACK) { return (size_t)(STACK + 1) * kBlock * sizeof(uint32_t); }
 
-template <int STACK, bool FAST, bool COUNT>
+template <int STACK, bool FAST, bool COUNT, int TK = -1>
 __device__ __forceinline__ int64_t trace(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
                                          Counters& c, double& t_best, int32_t& mat_best) {
 #if RTX_BVH4
 #if RTX_NODE_LEAN
-  if (FAST) return trace_fast4_lean<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best, mat_best);
+  if (FAST) return trace_fast4_lean<STACK, COUNT, TK>(S, o, d, tmin, tmax, stk, kBlock, c, t_best, mat_best);
 #else
   if (FAST) return trace_fast4<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best, mat_best);
 #endif
@@ -308,9 +308,9 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in,
 #endif
 constexpr int kChunk = RTX_CHUNK;
 
-// TK >= 0 (PARK schedule only): every primitive in the fast tree has kind TK (the bunny: the
-// ground sphere is a global primitive, the tree holds triangles), so the walk's leaf tests
-// are compiled for that kind alone.
+// TK >= 0: every primitive in the fast tree has kind TK (the ground sphere is a global
+// primitive, so the bunny's tree holds triangles, the final and mixed scenes' spheres), so
+// the walk's leaf tests are compiled for that kind alone.
 template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK = -1>
 __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderArgs A, unsigned long long* next_slot) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -426,7 +426,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
       } else if (kPark) {  // no BVH, or its root is a leaf
         best = trace_flat(A.S, P.o, P.d, tmin, kInf, c, COUNT, tb, bmat);
       } else {
-        best = trace<STACK, FAST, COUNT>(A.S, P.o, P.d, tmin, kInf, stk, c, tb, bmat);
+        best = trace<STACK, FAST, COUNT, TK>(A.S, P.o, P.d, tmin, kInf, stk, c, tb, bmat);
       }
       RTX_STAMP(1)
       segs++;
