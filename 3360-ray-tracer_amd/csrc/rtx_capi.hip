@@ -500,6 +500,10 @@ int persistent_grid(rtx_scene* sc, const void* fn, size_t lds) {
   return std::max(1, per_cu) * sc->cus;
 }
 
+#ifndef RTX_LAMB_KERNEL
+#define RTX_LAMB_KERNEL 1  // all-Lambertian scenes with a triangle tree: shading built for Lambertians only
+#endif
+
 struct Launch {
   rtx_scene* sc;
   hipStream_t s;
@@ -519,12 +523,13 @@ int run_extend(const Launch& L, const RenderArgs& A, const PathQueue& q, const u
   return RTX_OK;
 }
 
-template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK>
+template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK, bool LAMB = false>
 int run_persistent_k(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
   const size_t lds = stack_lds_bytes(STACK);
-  const int grid = persistent_grid(L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK>, lds);
-  hipLaunchKernelGGL((k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK>), dim3(grid), dim3(kBlock), lds, L.s, A,
-                     next_slot);
+  const int grid =
+      persistent_grid(L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB>, lds);
+  hipLaunchKernelGGL((k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB>), dim3(grid), dim3(kBlock), lds,
+                     L.s, A, next_slot);
   HIPC(hipGetLastError());
   return RTX_OK;
 }
@@ -534,7 +539,12 @@ template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK>
 int run_persistent(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
   constexpr bool spec = FAST && !COUNT && !SCATTER && RTX_TREE_KIND;
   constexpr int TK = spec ? (PARK ? (int)RTX_PRIM_TRIANGLE : (int)RTX_PRIM_SPHERE) : -1;
-  if (TK >= 0 && A.S.tree_kind == TK) return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK>(L, A, next_slot);
+  if (TK >= 0 && A.S.tree_kind == TK) {
+    // the triangle (PARK) build also comes for all-Lambertian scenes (the bunny)
+    if (TK == (int)RTX_PRIM_TRIANGLE && RTX_LAMB_KERNEL && A.S.all_lambertian)
+      return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK, TK == (int)RTX_PRIM_TRIANGLE>(L, A, next_slot);
+    return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK>(L, A, next_slot);
+  }
   return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, -1>(L, A, next_slot);
 }
 
@@ -722,6 +732,9 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   S.froot_leaf = 0, S.froot_count = 0;
   S.has_tris = 0;
   S.n_global = sc->fast_ok ? n_global : 0;
+  S.all_lambertian = d->n_materials > 0 ? 1 : 0;
+  for (int32_t i = 0; i < d->n_materials && S.all_lambertian; i++)
+    S.all_lambertian = d->materials[i].kind == RTX_MAT_LAMBERTIAN;
   S.tree_kind = -1;
   if (sc->fast_ok && d->n_prims > 0) {  // the one kind of the tree's primitives (globals excluded)
     int k = -2;

@@ -222,6 +222,7 @@ struct DScene {
   int32_t froot_count;
   int32_t has_tris;  // any triangle: prim_t preloads all 80 record bytes, else the first 48
   int32_t tree_kind;  // fast BVH: the one kind of every primitive in the tree, or -1
+  int32_t all_lambertian;  // every material is a Lambertian
   int32_t n_global;   // fast BVH: primitives kept out of the tree, tested before every walk
   int32_t global[2];  // their indices into prims (see build_global_prims, rtx_capi.hip)
 };
@@ -1347,6 +1348,9 @@ __device__ __forceinline__ V3 normalize_l(V3 v, double& l) {
 // Dielectric uses win = -normalize(wo) = normalize(normalize(d)) exactly (sign-symmetric
 // rounding), and eta = 1/ri (front face) / r0 = ((1-ri)/(1+ri))^2 precomputed at upload
 // in the same IEEE double operations (device material table, rtx_scene_create).
+// LAMB: every material of the scene is Lambertian (DScene::all_lambertian; the bunny), so the
+// metal / dielectric / emitter branches are compiled out.  Same operations for a Lambertian.
+template <bool LAMB = false>
 __device__ __forceinline__ bool shade_merged(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit,
                                              Rng& g, V3& L, const rtx_material& m) {
   L = v3(0, 0, 0);
@@ -1357,12 +1361,14 @@ __device__ __forceinline__ bool shade_merged(const DScene& S, int max_depth, Pat
     L = L + p.thr * ((1.0 - t) * v3(1.0, 1.0, 1.0) + t * v3(0.5, 0.7, 1.0));
     return false;
   }
-  V3 em = mat_emitted(S, m, rec);
-  if (!near_zero(em)) {
-    L = L + p.thr * em;
-    return false;
+  if (!LAMB) {  // Lambertian emits nothing (Material::Emitted default, material.h:50-54)
+    V3 em = mat_emitted(S, m, rec);
+    if (!near_zero(em)) {
+      L = L + p.thr * em;
+      return false;
+    }
   }
-  const int kind = m.kind;
+  const int kind = LAMB ? (int)RTX_MAT_LAMBERTIAN : m.kind;
   const bool isL = kind == RTX_MAT_LAMBERTIAN, isM = kind == RTX_MAT_METAL, isG = kind == RTX_MAT_DIELECTRIC;
   if (!(isL || isM || isG)) return false;  // DiffuseLight::Sample
   const V3 n = rec.normal;
@@ -1504,10 +1510,11 @@ __device__ __forceinline__ bool shade_by_material(const DScene& S, int max_depth
 }
 
 
+template <bool LAMB = false>
 __device__ __forceinline__ bool shade(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit, Rng& g,
                                       V3& L, const rtx_material& m) {
 #if RTX_MERGED_SHADE
-  return shade_merged(S, max_depth, p, rec, hit, g, L, m);
+  return shade_merged<LAMB>(S, max_depth, p, rec, hit, g, L, m);
 #else
   return shade_by_material(S, max_depth, p, rec, hit, g, L, m);
 #endif

@@ -311,7 +311,7 @@ constexpr int kChunk = RTX_CHUNK;
 // TK >= 0: every primitive in the fast tree has kind TK (the ground sphere is a global
 // primitive, so the bunny's tree holds triangles, the final and mixed scenes' spheres), so
 // the walk's leaf tests are compiled for that kind alone.
-template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK = -1>
+template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK = -1, bool LAMB = false>
 __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderArgs A, unsigned long long* next_slot) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* stk = lds + threadIdx.x;
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
           }
         }
       } else {
-        cont = shade(A.S, A.max_depth, P, h, best >= 0, g, L, m);
+        cont = shade<LAMB>(A.S, A.max_depth, P, h, best >= 0, g, L, m);
       }
     }
     RTX_STAMP(2)
@@ -498,9 +498,11 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
   extern template __global__ void k_persistent<ST, true, CO, SC, true>(RenderArgs, unsigned long long*);
 RTX_PARK_INSTANCES(RTX_PARK_EXTERN)
 #undef RTX_PARK_EXTERN
-#define RTX_PARK_TRI_EXTERN(ST) \
-  extern template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE>(RenderArgs, \
-                                                                                              unsigned long long*);
+#define RTX_PARK_TRI_EXTERN(ST)                                                                        \
+  extern template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE, false>(  \
+      RenderArgs, unsigned long long*);                                                                   \
+  extern template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE, true>(   \
+      RenderArgs, unsigned long long*);
 RTX_PARK_TRI_INSTANCES(RTX_PARK_TRI_EXTERN)
 #undef RTX_PARK_TRI_EXTERN
 #endif

@@ -13,9 +13,11 @@ namespace rtxd {
   template __global__ void k_persistent<ST, true, CO, SC, true>(RenderArgs, unsigned long long*);
 RTX_PARK_INSTANCES(RTX_PARK_DEFINE)
 #undef RTX_PARK_DEFINE
-#define RTX_PARK_TRI_DEFINE(ST) \
-  template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE>(RenderArgs, \
-                                                                                       unsigned long long*);
+#define RTX_PARK_TRI_DEFINE(ST)                                                                              \
+  template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE, false>(RenderArgs,     \
+                                                                                              unsigned long long*); \
+  template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE, true>(RenderArgs,      \
+                                                                                             unsigned long long*);
 RTX_PARK_TRI_INSTANCES(RTX_PARK_TRI_DEFINE)
 #undef RTX_PARK_TRI_DEFINE
 }  // namespace rtxd
