@@ -500,6 +500,9 @@ int persistent_grid(rtx_scene* sc, const void* fn, size_t lds) {
   return std::max(1, per_cu) * sc->cus;
 }
 
+#ifndef RTX_NOTEX_KERNEL
+#define RTX_NOTEX_KERNEL 1  // texture-free scenes with a sphere tree: shading without texture lookups
+#endif
 #ifndef RTX_LAMB_KERNEL
 #define RTX_LAMB_KERNEL 1  // all-Lambertian scenes with a triangle tree: shading built for Lambertians only
 #endif
@@ -523,13 +526,13 @@ int run_extend(const Launch& L, const RenderArgs& A, const PathQueue& q, const u
   return RTX_OK;
 }
 
-template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK, bool LAMB = false>
+template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK, bool LAMB = false, bool NOTEX = false>
 int run_persistent_k(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
   const size_t lds = stack_lds_bytes(STACK);
   const int grid =
-      persistent_grid(L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB>, lds);
-  hipLaunchKernelGGL((k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB>), dim3(grid), dim3(kBlock), lds,
-                     L.s, A, next_slot);
+      persistent_grid(L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX>, lds);
+  hipLaunchKernelGGL((k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX>), dim3(grid), dim3(kBlock),
+                     lds, L.s, A, next_slot);
   HIPC(hipGetLastError());
   return RTX_OK;
 }
@@ -543,6 +546,10 @@ int run_persistent(const Launch& L, const RenderArgs& A, unsigned long long* nex
     // the triangle (PARK) build also comes for all-Lambertian scenes (the bunny)
     if (TK == (int)RTX_PRIM_TRIANGLE && RTX_LAMB_KERNEL && A.S.all_lambertian)
       return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK, TK == (int)RTX_PRIM_TRIANGLE>(L, A, next_slot);
+    // the sphere (plain) build also comes for scenes that read no textures (the final scene)
+    if (TK == (int)RTX_PRIM_SPHERE && RTX_NOTEX_KERNEL && A.S.no_textures)
+      return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK, false, TK == (int)RTX_PRIM_SPHERE>(L, A,
+                                                                                                       next_slot);
     return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK>(L, A, next_slot);
   }
   return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, -1>(L, A, next_slot);
@@ -735,6 +742,9 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   S.all_lambertian = d->n_materials > 0 ? 1 : 0;
   for (int32_t i = 0; i < d->n_materials && S.all_lambertian; i++)
     S.all_lambertian = d->materials[i].kind == RTX_MAT_LAMBERTIAN;
+  S.no_textures = 1;
+  for (const rtx_material& m : dmats)
+    if ((m.kind == RTX_MAT_LAMBERTIAN || m.kind == RTX_MAT_DIFFUSE_LIGHT) && m.texture >= 0) S.no_textures = 0;
   S.tree_kind = -1;
   if (sc->fast_ok && d->n_prims > 0) {  // the one kind of the tree's primitives (globals excluded)
     int k = -2;

@@ -223,6 +223,7 @@ struct DScene {
   int32_t has_tris;  // any triangle: prim_t preloads all 80 record bytes, else the first 48
   int32_t tree_kind;  // fast BVH: the one kind of every primitive in the tree, or -1
   int32_t all_lambertian;  // every material is a Lambertian
+  int32_t no_textures;     // no material reads the texture table (solid colours resolved at upload)
   int32_t n_global;   // fast BVH: primitives kept out of the tree, tested before every walk
   int32_t global[2];  // their indices into prims (see build_global_prims, rtx_capi.hip)
 };
@@ -1281,6 +1282,19 @@ __device__ __forceinline__ V3 mat_emitted(const DScene& S, const rtx_material& m
   if (m.kind == RTX_MAT_DIFFUSE_LIGHT) return mat_tex(S, m, rec);
   return v3(0, 0, 0);
 }
+// NOTEX: no material of the scene reads a texture table entry (DScene::no_textures: every
+// Lambertian / DiffuseLight colour was resolved into the device material table), so the
+// texture lookup is compiled out.
+template <bool NOTEX>
+__device__ __forceinline__ V3 mat_tex_t(const DScene& S, const rtx_material& m, const Hit& rec) {
+  if (NOTEX) return v3(m.albedo[0], m.albedo[1], m.albedo[2]);
+  return mat_tex(S, m, rec);
+}
+template <bool NOTEX>
+__device__ __forceinline__ V3 mat_emitted_t(const DScene& S, const rtx_material& m, const Hit& rec) {
+  if (m.kind == RTX_MAT_DIFFUSE_LIGHT) return mat_tex_t<NOTEX>(S, m, rec);
+  return v3(0, 0, 0);
+}
 
 __device__ __forceinline__ V3 sky(V3 d) {  // wavefront.cc:33-38, camera.h:171-173
   V3 ud = normalize(d);
@@ -1350,7 +1364,7 @@ __device__ __forceinline__ V3 normalize_l(V3 v, double& l) {
 // in the same IEEE double operations (device material table, rtx_scene_create).
 // LAMB: every material of the scene is Lambertian (DScene::all_lambertian; the bunny), so the
 // metal / dielectric / emitter branches are compiled out.  Same operations for a Lambertian.
-template <bool LAMB = false>
+template <bool LAMB = false, bool NOTEX = false>
 __device__ __forceinline__ bool shade_merged(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit,
                                              Rng& g, V3& L, const rtx_material& m) {
   L = v3(0, 0, 0);
@@ -1362,7 +1376,7 @@ __device__ __forceinline__ bool shade_merged(const DScene& S, int max_depth, Pat
     return false;
   }
   if (!LAMB) {  // Lambertian emits nothing (Material::Emitted default, material.h:50-54)
-    V3 em = mat_emitted(S, m, rec);
+    V3 em = mat_emitted_t<NOTEX>(S, m, rec);
     if (!near_zero(em)) {
       L = L + p.thr * em;
       return false;
@@ -1442,7 +1456,7 @@ __device__ __forceinline__ bool shade_merged(const DScene& S, int max_depth, Pat
     if (dot(wi, n) <= 0) return false;
     const float cf = (float)dot(n, wi);
     const float pdf = (cf <= 0.0f) ? 0.0f : (float)((double)cf / kPi);
-    f = mat_tex(S, m, rec) / kPi;
+    f = mat_tex_t<NOTEX>(S, m, rec) / kPi;
     if (pdf < 1e-6f) return false;
     const float ct = fmaxf(0.0f, (float)dot(wi, n));
     c.thr = ((double)ct * (p.thr * f)) / (double)pdf;
@@ -1510,11 +1524,11 @@ __device__ __forceinline__ bool shade_by_material(const DScene& S, int max_depth
 }
 
 
-template <bool LAMB = false>
+template <bool LAMB = false, bool NOTEX = false>
 __device__ __forceinline__ bool shade(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit, Rng& g,
                                       V3& L, const rtx_material& m) {
 #if RTX_MERGED_SHADE
-  return shade_merged<LAMB>(S, max_depth, p, rec, hit, g, L, m);
+  return shade_merged<LAMB, NOTEX>(S, max_depth, p, rec, hit, g, L, m);
 #else
   return shade_by_material(S, max_depth, p, rec, hit, g, L, m);
 #endif

@@ -311,7 +311,8 @@ constexpr int kChunk = RTX_CHUNK;
 // TK >= 0: every primitive in the fast tree has kind TK (the ground sphere is a global
 // primitive, so the bunny's tree holds triangles, the final and mixed scenes' spheres), so
 // the walk's leaf tests are compiled for that kind alone.
-template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK = -1, bool LAMB = false>
+template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK = -1, bool LAMB = false,
+          bool NOTEX = false>
 __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderArgs A, unsigned long long* next_slot) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* stk = lds + threadIdx.x;
@@ -462,7 +463,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
           }
         }
       } else {
-        cont = shade<LAMB>(A.S, A.max_depth, P, h, best >= 0, g, L, m);
+        cont = shade<LAMB, NOTEX>(A.S, A.max_depth, P, h, best >= 0, g, L, m);
       }
     }
     RTX_STAMP(2)
