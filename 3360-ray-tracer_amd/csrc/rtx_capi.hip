@@ -544,8 +544,12 @@ int run_persistent(const Launch& L, const RenderArgs& A, unsigned long long* nex
   constexpr int TK = spec ? (PARK ? (int)RTX_PRIM_TRIANGLE : (int)RTX_PRIM_SPHERE) : -1;
   if (TK >= 0 && A.S.tree_kind == TK) {
     // the triangle (PARK) build also comes for all-Lambertian scenes (the bunny)
-    if (TK == (int)RTX_PRIM_TRIANGLE && RTX_LAMB_KERNEL && A.S.all_lambertian)
-      return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK, TK == (int)RTX_PRIM_TRIANGLE>(L, A, next_slot);
+    if (TK == (int)RTX_PRIM_TRIANGLE && RTX_LAMB_KERNEL && A.S.all_lambertian) {
+      constexpr bool tri = TK == (int)RTX_PRIM_TRIANGLE;
+      if (RTX_NOTEX_KERNEL && A.S.no_textures)
+        return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK, tri, tri>(L, A, next_slot);
+      return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK, tri>(L, A, next_slot);
+    }
     // the sphere (plain) build also comes for scenes that read no textures (the final scene)
     if (TK == (int)RTX_PRIM_SPHERE && RTX_NOTEX_KERNEL && A.S.no_textures)
       return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK, false, TK == (int)RTX_PRIM_SPHERE>(L, A,

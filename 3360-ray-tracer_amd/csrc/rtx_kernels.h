@@ -503,6 +503,8 @@ RTX_PARK_INSTANCES(RTX_PARK_EXTERN)
   extern template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE, false>(  \
       RenderArgs, unsigned long long*);                                                                   \
   extern template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE, true>(   \
+      RenderArgs, unsigned long long*);                                                                   \
+  extern template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE, true, true>( \
       RenderArgs, unsigned long long*);
 RTX_PARK_TRI_INSTANCES(RTX_PARK_TRI_EXTERN)
 #undef RTX_PARK_TRI_EXTERN

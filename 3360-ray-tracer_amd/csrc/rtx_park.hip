@@ -17,7 +17,9 @@ RTX_PARK_INSTANCES(RTX_PARK_DEFINE)
   template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE, false>(RenderArgs,     \
                                                                                               unsigned long long*); \
   template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE, true>(RenderArgs,      \
-                                                                                             unsigned long long*);
+                                                                                             unsigned long long*); \
+  template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE, true, true>(             \
+      RenderArgs, unsigned long long*);
 RTX_PARK_TRI_INSTANCES(RTX_PARK_TRI_DEFINE)
 #undef RTX_PARK_TRI_DEFINE
 }  // namespace rtxd
