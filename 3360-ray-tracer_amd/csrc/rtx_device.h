@@ -1118,7 +1118,8 @@ template <int STACK, bool COUNT, int KIND = -1>
 __device__ __forceinline__ int64_t trace_fast4_lean(const DScene& S, V3 o, V3 d, double tmin, double tmax,
                                                     uint32_t* stk, int stride, Counters& cnt, double& t_best,
                                                     int32_t& mat_best) {
-  if (!S.use_bvh || S.froot_leaf) return trace_flat(S, o, d, tmin, tmax, cnt, COUNT, t_best, mat_best);
+  // KIND >= 0 builds run only on scenes with a fast tree (an internal root): no flat list
+  if (KIND < 0 && (!S.use_bvh || S.froot_leaf)) return trace_flat(S, o, d, tmin, tmax, cnt, COUNT, t_best, mat_best);
   TravState ts;
   trav_init(ts, tmax);
   trav_globals<COUNT>(S, o, d, tmin, cnt, ts);
