@@ -1304,6 +1304,9 @@ __device__ __forceinline__ V3 sky(V3 d) {  // wavefront.cc:33-38, camera.h:171-1
 }
 
 // Camera::GetRay (camera.h:134-144,196-203): y offset drawn first (g++ arg order).
+// NODOF: the camera has no defocus (the host checked defocus_angle <= 0), so the thin-lens
+// sampling is compiled out.
+template <bool NODOF = false>
 __device__ __forceinline__ void get_ray(const rtx_camera& c, int i, int j, Rng& g, V3& o, V3& d) {
   double oy = g.next() - 0.5;
   double ox = g.next() - 0.5;
@@ -1312,7 +1315,7 @@ __device__ __forceinline__ void get_ray(const rtx_camera& c, int i, int j, Rng& 
   V3 dv{c.pixel_delta_v[0], c.pixel_delta_v[1], c.pixel_delta_v[2]};
   V3 ps = p00 + ((i + ox) * du) + ((j + oy) * dv);
   V3 center{c.center[0], c.center[1], c.center[2]};
-  if (c.defocus_angle <= 0) {
+  if (NODOF || c.defocus_angle <= 0) {
     o = center;
   } else {
     V3 p = random_in_unit_disk(g);

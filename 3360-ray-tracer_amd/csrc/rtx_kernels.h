@@ -312,7 +312,7 @@ constexpr int kChunk = RTX_CHUNK;
 // primitive, so the bunny's tree holds triangles, the final and mixed scenes' spheres), so
 // the walk's leaf tests are compiled for that kind alone.
 template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK = -1, bool LAMB = false,
-          bool NOTEX = false>
+          bool NOTEX = false, bool NODOF = false>
 __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderArgs A, unsigned long long* next_slot) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* stk = lds + threadIdx.x;
@@ -389,7 +389,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
         A.map.xy(p, x, y);
         pix = (uint32_t)(y * A.map.W + x), smp = (uint32_t)(A.s0 + k);
         Rng g = make_rng(A.seed, pix, smp, 0u);
-        get_ray(A.cam, x, y, g, P.o, P.d);
+        get_ray<NODOF>(A.cam, x, y, g, P.o, P.d);
         P.thr = v3(1.0, 1.0, 1.0);
         P.depth = SCATTER ? A.max_depth : 0;
         has = true;
