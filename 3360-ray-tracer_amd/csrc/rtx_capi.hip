@@ -9,6 +9,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "rtx.h"
@@ -57,6 +58,25 @@ struct DevBuf {
   }
 };
 
+struct HostBuf {  // pinned host staging (grow-only)
+  void* p = nullptr;
+  size_t n = 0;
+  int reserve(size_t bytes) {
+    if (bytes <= n) return RTX_OK;
+    if (p) (void)hipHostFree(p);
+    p = nullptr, n = 0;
+    if (bytes == 0) return RTX_OK;
+    hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+    if (e != hipSuccess) return fail(RTX_ERR_NOMEM, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    n = bytes;
+    return RTX_OK;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr, n = 0;
+  }
+};
+
 float round_down(double x) {
   float f = (float)x;
   if ((double)f > x) f = std::nextafter(f, -INFINITY);
@@ -85,6 +105,7 @@ struct rtx_scene {
   // render workspace (grow-only)
   DevBuf px_sum, px_mean, px_m2, px_samples, px_conv, lbuf, queue[2], counters, out_rgb, out_spp, rays, hits;
   DevBuf p3_scratch, p3_body;  // device P3 encoding (rtx_p3.h)
+  HostBuf stage_rgb, stage_spp;  // rtx_render_multi: pinned D2H staging of this device's stripes
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> evpool;
   ~rtx_scene() {
@@ -95,6 +116,7 @@ struct rtx_scene {
                       &p3_body, &calib_rgb})
       b->release();
     for (auto& t : texels) t.release();
+    stage_rgb.release(), stage_spp.release();
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
     if (stream) (void)hipStreamDestroy(stream);
@@ -516,6 +538,8 @@ struct Launch {
   int stack;
   bool fast, count;
   bool park = false;  // persistent: the PARK kernel (parked traversals), chosen per scene
+  bool generic = false;  // RTX_FLAG_GENERIC: no per-scene specialisation (TK, LAMB, NOTEX, NODOF)
+  mutable uint32_t build = 0;  // RTX_BUILD_* bits of the persistent instantiation launched last
 };
 
 template <int STACK, bool FAST, bool COUNT>
@@ -535,6 +559,10 @@ int run_persistent_k0(const Launch& L, const RenderArgs& A, unsigned long long* 
   const size_t lds = stack_lds_bytes(STACK);
   const int grid = persistent_grid(
       L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF>, lds);
+  L.build = (PARK ? RTX_BUILD_PARK : 0u) | (TK == (int)RTX_PRIM_SPHERE ? RTX_BUILD_SPHERE_TREE : 0u) |
+            (TK == (int)RTX_PRIM_TRIANGLE ? RTX_BUILD_TRIANGLE_TREE : 0u) | (LAMB ? RTX_BUILD_LAMBERTIAN : 0u) |
+            (NOTEX ? RTX_BUILD_NO_TEXTURES : 0u) | (NODOF ? RTX_BUILD_NO_DEFOCUS : 0u) |
+            (FAST ? RTX_BUILD_FAST : 0u) | (COUNT ? RTX_BUILD_COUNT : 0u) | (SCATTER ? RTX_BUILD_SCATTER : 0u);
   hipLaunchKernelGGL((k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF>), dim3(grid),
                      dim3(kBlock), lds, L.s, A, next_slot);
   HIPC(hipGetLastError());
@@ -554,7 +582,7 @@ template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK>
 int run_persistent(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
   constexpr bool spec = FAST && !COUNT && !SCATTER && RTX_TREE_KIND;
   constexpr int TK = spec ? (PARK ? (int)RTX_PRIM_TRIANGLE : (int)RTX_PRIM_SPHERE) : -1;
-  if (TK >= 0 && A.S.tree_kind == TK) {
+  if (TK >= 0 && A.S.tree_kind == TK && !L.generic) {
     // the triangle (PARK) build also comes for all-Lambertian scenes (the bunny)
     if (TK == (int)RTX_PRIM_TRIANGLE && RTX_LAMB_KERNEL && A.S.all_lambertian) {
       constexpr bool tri = TK == (int)RTX_PRIM_TRIANGLE;
@@ -594,7 +622,7 @@ int persist_m(const Launch& L, const RenderArgs& A, unsigned long long* ns) {
   return L.count ? persist_s<false, true, SCATTER, false>(L, A, ns) : persist_s<false, false, SCATTER, false>(L, A, ns);
 }
 
-int time_park_schedule(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm);
+int time_park_schedule(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm, hipStream_t s);
 
 }  // namespace
 
@@ -622,6 +650,10 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   if (d->n_prims < 0 || d->n_nodes < 0 || d->n_materials < 0 || d->n_textures < 0 || d->n_images < 0)
     return fail(RTX_ERR_INVALID, "negative counts");
   if (d->n_prims > 0 && !d->prims) return fail(RTX_ERR_INVALID, "prims is NULL");
+  if (d->n_materials > 0 && !d->materials) return fail(RTX_ERR_INVALID, "materials is NULL");
+  if (d->n_textures > 0 && !d->textures) return fail(RTX_ERR_INVALID, "textures is NULL");
+  if (d->n_images > 0 && !d->images) return fail(RTX_ERR_INVALID, "images is NULL");
+  if (d->n_nodes > 0 && !d->nodes) return fail(RTX_ERR_INVALID, "nodes is NULL");
   if (d->n_prims > 0x7FFFFFFFll) return fail(RTX_ERR_INVALID, "more than 2^31-1 primitives");
   // validate indices so kernels never read out of bounds
   for (int64_t i = 0; i < d->n_prims; i++) {
@@ -637,9 +669,16 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   }
   for (int32_t i = 0; i < d->n_textures; i++) {
     const rtx_texture& t = d->textures[i];
+    // the device treats every kind other than solid / checker as an image lookup
+    if (t.kind < RTX_TEX_SOLID || t.kind > RTX_TEX_IMAGE) return fail(RTX_ERR_INVALID, "bad texture kind");
     if (t.kind == RTX_TEX_CHECKER && (t.even < 0 || t.even >= d->n_textures || t.odd < 0 || t.odd >= d->n_textures))
       return fail(RTX_ERR_INVALID, "checker child out of range");
     if (t.kind == RTX_TEX_IMAGE && t.image >= d->n_images) return fail(RTX_ERR_INVALID, "image index out of range");
+  }
+  for (int32_t i = 0; i < d->n_images; i++) {
+    const rtx_image& im = d->images[i];
+    if (im.width < 0 || im.height < 0) return fail(RTX_ERR_INVALID, "negative image size");
+    if ((int64_t)im.width * im.height > (1ll << 31)) return fail(RTX_ERR_INVALID, "image above 2^31 texels");
   }
   for (int64_t i = 0; i < d->n_nodes; i++) {
     const rtx_bvh_node& n = d->nodes[i];
@@ -894,12 +933,13 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
   hipStream_t s = stream ? (hipStream_t)stream : sc->stream;
   const bool fast = prm->precision == RTX_PREC_FAST && sc->fast_ok;
   Launch L{sc, s, fast ? sc->stack_fast : sc->stack_parity, fast, (prm->flags & RTX_FLAG_COUNT) != 0};
+  L.generic = (prm->flags & RTX_FLAG_GENERIC) != 0;
   if (fast && prm->mode == RTX_MODE_PERSISTENT && RTX_PARK > 0) {
     if (prm->flags & RTX_FLAG_PARK) L.park = true;
     else if (prm->flags & RTX_FLAG_NO_PARK) L.park = false;
     else {
       int rc;
-      if (sc->park < 0 && (rc = time_park_schedule(sc, cam, prm))) return rc;
+      if (sc->park < 0 && (rc = time_park_schedule(sc, cam, prm, s))) return rc;
       L.park = sc->park == 1;
     }
   }
@@ -1064,6 +1104,7 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
     stats->wave_prim_iters = h[5];
     stats->tri_tests = h[6];
     stats->sphere_tests = h[7];
+    stats->build = prm->mode == RTX_MODE_WAVEFRONT ? 0 : L.build;
     stats->node_bytes = (L.fast && RTX_BVH4) ? sizeof(F4Node) : (L.fast ? sizeof(FNode) : sizeof(rtx_bvh_node));
 #if RTX_TAILHIST
     if (h[4]) {
@@ -1104,6 +1145,117 @@ int rtx_render(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* pr
   return RTX_OK;
 }
 
+// ---- one frame over several devices (wavefront.cc:228-241's one framebuffer) ----
+namespace {
+// Device k renders stripe (first + k) of `count` interleaved stripes; its packed stripe rows
+// come back over one D2H copy (pinned staging, or a 2D copy straight into a pinned caller
+// buffer) and are placed at their rows of the whole-frame buffers.
+int render_stripes_to_host(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* base, int stripe,
+                           double* out_rgb, int32_t* out_spp, rtx_stats* st) {
+  rtx_render_params q = *base;
+  q.stripe_index = stripe;
+  q.x0 = q.y0 = q.w = q.h = 0;
+  PixelMap map;
+  std::string err;
+  const int64_t npix = subset_pixels(cam, &q, map, err);
+  if (npix < 0) return fail(RTX_ERR_INVALID, err);
+  HIPC(hipSetDevice(sc->device));
+  int rc;
+  if ((rc = sc->out_rgb.reserve(std::max<int64_t>(1, npix) * 3 * sizeof(double)))) return rc;
+  if ((rc = sc->out_spp.reserve(std::max<int64_t>(1, npix) * sizeof(int32_t)))) return rc;
+  if ((rc = rtx_render_device(sc, cam, &q, sc->out_rgb.as<double>(), sc->out_spp.as<int32_t>(), st, sc->stream)))
+    return rc;
+  if (npix == 0) return RTX_OK;
+  const int64_t W = map.W, H = map.H, R = map.srows, N = map.scount;
+  const int64_t nblk = (H + R - 1) / R;  // stripes of the image; ours: stripe, stripe + N, ...
+  const size_t row_rgb = (size_t)W * 3 * sizeof(double), row_spp = (size_t)W * sizeof(int32_t);
+  hipPointerAttribute_t at{};
+  const bool pinned = hipPointerGetAttributes(&at, out_rgb) == hipSuccess && at.type == hipMemoryTypeHost;
+  (void)hipGetLastError();  // pageable memory reports an error here on some runtimes
+  const int64_t full = (H / R > stripe) ? (H / R - stripe + N - 1) / N : 0;  // our stripes with R rows
+  if (pinned && full > 0) {  // whole stripes in one strided DMA, the short last stripe after it
+    HIPC(hipMemcpy2DAsync(out_rgb + (size_t)stripe * R * W * 3, (size_t)N * R * row_rgb, sc->out_rgb.p,
+                          (size_t)R * row_rgb, (size_t)R * row_rgb, (size_t)full, hipMemcpyDeviceToHost, sc->stream));
+    const int64_t rest = npix / W - full * R;
+    if (rest > 0)
+      HIPC(hipMemcpyAsync(out_rgb + (size_t)((stripe + full * N) * R) * W * 3,
+                          sc->out_rgb.as<double>() + (size_t)full * R * W * 3, (size_t)rest * row_rgb,
+                          hipMemcpyDeviceToHost, sc->stream));
+  } else {
+    if ((rc = sc->stage_rgb.reserve((size_t)npix * 3 * sizeof(double)))) return rc;
+    HIPC(hipMemcpyAsync(sc->stage_rgb.p, sc->out_rgb.p, (size_t)npix * 3 * sizeof(double), hipMemcpyDeviceToHost,
+                        sc->stream));
+  }
+  if (out_spp) {
+    if ((rc = sc->stage_spp.reserve((size_t)npix * sizeof(int32_t)))) return rc;
+    HIPC(hipMemcpyAsync(sc->stage_spp.p, sc->out_spp.p, (size_t)npix * sizeof(int32_t), hipMemcpyDeviceToHost,
+                        sc->stream));
+  }
+  HIPC(hipStreamSynchronize(sc->stream));
+  int64_t r = 0;  // packed row
+  for (int64_t b = stripe; b < nblk; b += N) {
+    const int64_t y0 = b * R, rows = std::min<int64_t>(R, H - y0);
+    if (!pinned || full == 0)
+      std::memcpy(out_rgb + (size_t)y0 * W * 3, (const char*)sc->stage_rgb.p + (size_t)r * row_rgb,
+                  (size_t)rows * row_rgb);
+    if (out_spp)
+      std::memcpy(out_spp + (size_t)y0 * W, (const char*)sc->stage_spp.p + (size_t)r * row_spp,
+                  (size_t)rows * row_spp);
+    r += rows;
+  }
+  return RTX_OK;
+}
+}  // namespace
+
+int rtx_render_multi(rtx_scene* const* scenes, int32_t n, const rtx_camera* cam, const rtx_render_params* prm,
+                     double* out_rgb, int32_t* out_spp, rtx_stats* stats, rtx_stats* per_scene) {
+  if (!scenes || n <= 0 || !cam || !prm || !out_rgb) return fail(RTX_ERR_INVALID, "bad argument");
+  for (int32_t k = 0; k < n; k++)
+    if (!scenes[k]) return fail(RTX_ERR_INVALID, "scene is NULL");
+  for (int32_t j = 0; j < n; j++)
+    for (int32_t k = j + 1; k < n; k++)
+      if (scenes[j] == scenes[k]) return fail(RTX_ERR_INVALID, "a scene appears twice (one scene per render thread)");
+  rtx_render_params base = *prm;
+  if (base.stripe_rows <= 0) base.stripe_rows = 8;
+  if (base.stripe_count <= 0) base.stripe_count = n, base.stripe_index = 0;
+  if (base.stripe_index < 0 || base.stripe_index + n > base.stripe_count)
+    return fail(RTX_ERR_INVALID, "stripes stripe_index .. stripe_index + n - 1 must lie below stripe_count");
+  std::vector<int> rc(n, RTX_OK);
+  std::vector<std::string> msg(n);
+  std::vector<rtx_stats> st(n);
+  auto work = [&](int k) {
+    st[k] = rtx_stats{};
+    rc[k] = render_stripes_to_host(scenes[k], cam, &base, base.stripe_index + k, out_rgb, out_spp, &st[k]);
+    if (rc[k] != RTX_OK) msg[k] = g_err;  // rtx_last_error is per thread
+  };
+  if (n == 1) {
+    work(0);
+  } else {
+    std::vector<std::thread> th;
+    th.reserve(n);
+    for (int k = 0; k < n; k++) th.emplace_back(work, k);
+    for (auto& t : th) t.join();
+  }
+  for (int k = 0; k < n; k++)
+    if (rc[k] != RTX_OK) return fail(rc[k], "device " + std::to_string(scenes[k]->device) + ": " + msg[k]);
+  if (per_scene)
+    for (int k = 0; k < n; k++) per_scene[k] = st[k];
+  if (stats) {
+    rtx_stats a{};
+    for (int k = 0; k < n; k++) {
+      a.rays_primary += st[k].rays_primary, a.rays_total += st[k].rays_total, a.paths += st[k].paths;
+      a.kernel_ms = std::max(a.kernel_ms, st[k].kernel_ms);
+      a.hot_kernel_ms = std::max(a.hot_kernel_ms, st[k].hot_kernel_ms);
+      a.hot_launches += st[k].hot_launches, a.node_visits += st[k].node_visits, a.prim_tests += st[k].prim_tests;
+      a.wave_node_iters += st[k].wave_node_iters, a.wave_prim_iters += st[k].wave_prim_iters;
+      a.tri_tests += st[k].tri_tests, a.sphere_tests += st[k].sphere_tests;
+      a.node_bytes = st[k].node_bytes, a.parked |= st[k].parked, a.build |= st[k].build;
+    }
+    *stats = a;
+  }
+  return RTX_OK;
+}
+
 // ---- P3 output on the device (wavefront.cc:238-241, core/color.h:18-33) ----
 static std::string p3_header(int64_t w, int64_t h) {
   return "P3\n" + std::to_string(w) + " " + std::to_string(h) + "\n255\n";
@@ -1137,6 +1289,24 @@ int rtx_encode_p3_device(rtx_scene* sc, const double* d_rgb, int32_t w, int32_t 
   HIPC(hipMemcpyAsync(d_out, hd.data(), hd.size(), hipMemcpyHostToDevice, s));
   HIPC(hipMemcpyAsync(d_out + hd.size(), sc->p3_body.p, body, hipMemcpyDeviceToDevice, s));
   HIPC(hipStreamSynchronize(s));
+  *out_len = hd.size() + body;
+  return RTX_OK;
+}
+
+int rtx_encode_p3(rtx_scene* sc, const double* rgb, int32_t w, int32_t h, char* out, size_t cap, size_t* out_len) {
+  if (!sc || !rgb || !out || !out_len || w <= 0 || h <= 0) return fail(RTX_ERR_INVALID, "bad argument");
+  if (cap < rtx_p3_max_bytes(w, h)) return fail(RTX_ERR_INVALID, "output buffer below rtx_p3_max_bytes");
+  HIPC(hipSetDevice(sc->device));
+  const int64_t npix = (int64_t)w * h;
+  int rc;
+  if ((rc = sc->out_rgb.reserve(npix * 3 * sizeof(double)))) return rc;
+  HIPC(hipMemcpyAsync(sc->out_rgb.p, rgb, npix * 3 * sizeof(double), hipMemcpyHostToDevice, sc->stream));
+  const std::string hd = p3_header(w, h);
+  size_t body = 0;
+  if ((rc = p3_encode(sc, sc->out_rgb.as<double>(), npix, &body, sc->stream))) return rc;
+  std::memcpy(out, hd.data(), hd.size());
+  HIPC(hipMemcpyAsync(out + hd.size(), sc->p3_body.p, body, hipMemcpyDeviceToHost, sc->stream));
+  HIPC(hipStreamSynchronize(sc->stream));
   *out_len = hd.size() + body;
   return RTX_OK;
 }
@@ -1197,12 +1367,14 @@ namespace {
 // results, so the choice is timing only: the first persistent fast render of a scene renders
 // a centre tile of 1/16 of its pixels with each kernel (twice each; the faster second run
 // counts) and keeps the one with the higher segment rate for the scene.
-int time_park_schedule(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm) {
+// The timing renders run on the caller's stream `s`, so they are ordered after any render
+// still queued there: they share the scene's scratch buffers (pixel state, Lbuf, counters).
+int time_park_schedule(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm, hipStream_t s) {
   rtx_render_params q = *prm;
   q.stripe_rows = q.stripe_index = q.stripe_count = 0;
   q.w = std::max(1, cam->image_width / 4), q.h = std::max(1, cam->image_height / 4);
   q.x0 = (cam->image_width - q.w) / 2, q.y0 = (cam->image_height - q.h) / 2;
-  q.flags = prm->flags & ~(RTX_FLAG_COUNT | RTX_FLAG_PARK | RTX_FLAG_NO_PARK);
+  q.flags = prm->flags & ~(RTX_FLAG_COUNT | RTX_FLAG_PARK | RTX_FLAG_NO_PARK | RTX_FLAG_GENERIC);
   int rc;
   if ((rc = sc->calib_rgb.reserve((size_t)q.w * q.h * 3 * sizeof(double)))) return rc;
   double rate[2] = {0, 0};
@@ -1211,7 +1383,7 @@ int time_park_schedule(rtx_scene* sc, const rtx_camera* cam, const rtx_render_pa
       rtx_render_params r = q;
       r.flags |= k ? RTX_FLAG_PARK : RTX_FLAG_NO_PARK;
       rtx_stats st{};
-      if ((rc = rtx_render_device(sc, cam, &r, sc->calib_rgb.as<double>(), nullptr, &st, nullptr))) return rc;
+      if ((rc = rtx_render_device(sc, cam, &r, sc->calib_rgb.as<double>(), nullptr, &st, s))) return rc;
       rate[k] = st.hot_kernel_ms > 0 ? (double)st.rays_total / st.hot_kernel_ms : 0.0;
     }
   sc->park = rate[1] > 1.02 * rate[0] ? 1 : 0;

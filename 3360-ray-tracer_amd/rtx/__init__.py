@@ -18,6 +18,15 @@ RTX_OK = 0
 RTX_SEAM_TMIN = float(np.float32(0.001))
 MODES = {"wavefront": 0, "persistent": 1, "megakernel": 2}
 PRECISIONS = {"parity": 0, "fast": 1}
+RTX_FLAG_COUNT, RTX_FLAG_PARK, RTX_FLAG_NO_PARK, RTX_FLAG_GENERIC = 1, 2, 4, 8
+SCHEDULE_FLAGS = {None: 0, "auto": 0, "park": RTX_FLAG_PARK, "plain": RTX_FLAG_NO_PARK}
+BUILD_BITS = {"park": 1, "sphere_tree": 2, "triangle_tree": 4, "lambertian": 8, "no_textures": 16,
+              "no_defocus": 32, "fast": 64, "count": 128, "scatter": 256}
+
+
+def build_names(bits):
+    """rtx_stats.build bits -> names of the persistent-kernel specialisations that ran."""
+    return [k for k, b in BUILD_BITS.items() if bits & b]
 
 
 class RtxError(RuntimeError):
@@ -91,7 +100,8 @@ class Stats(C.Structure):
                 ("kernel_ms", C.c_double), ("hot_kernel_ms", C.c_double), ("hot_launches", C.c_uint64),
                 ("node_visits", C.c_uint64), ("prim_tests", C.c_uint64),
                 ("node_bytes", C.c_uint64), ("wave_node_iters", C.c_uint64), ("wave_prim_iters", C.c_uint64),
-                ("tri_tests", C.c_uint64), ("sphere_tests", C.c_uint64), ("parked", C.c_uint64)]
+                ("tri_tests", C.c_uint64), ("sphere_tests", C.c_uint64), ("parked", C.c_uint64),
+                ("build", C.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -103,7 +113,7 @@ EXPORTS = ["rtx_abi_version", "rtx_last_error", "rtx_device_count", "rtx_scene_c
            "rtx_render_device", "rtx_host_scene_load", "rtx_host_scene_recipe", "rtx_host_scene_write",
            "rtx_host_scene_desc", "rtx_host_scene_prim_indices", "rtx_host_scene_destroy",
            "rtx_camera_config_load", "rtx_write_ppm", "rtx_p3_max_bytes", "rtx_render_p3", "rtx_encode_p3_device",
-           "rtx_prim_bounds", "rtx_bvh_build", "rtx_bvh_build_host"]
+           "rtx_prim_bounds", "rtx_bvh_build", "rtx_bvh_build_host", "rtx_render_multi", "rtx_encode_p3"]
 
 _lib = None
 
@@ -144,6 +154,9 @@ def lib():
             "rtx_prim_bounds": ([vp, i64, vp], C.c_int),
             "rtx_bvh_build": ([C.c_int, vp, i64, vp, C.POINTER(i64), vp], C.c_int),
             "rtx_bvh_build_host": ([vp, i64, vp, C.POINTER(i64), vp], C.c_int),
+            "rtx_render_multi": ([C.POINTER(vp), i32, C.POINTER(Camera), C.POINTER(RenderParams), vp, vp,
+                                  C.POINTER(Stats), vp], C.c_int),
+            "rtx_encode_p3": ([vp, vp, i32, i32, vp, sz, C.POINTER(sz)], C.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -274,13 +287,13 @@ class DeviceScene:
 
     def render(self, cam, spp, max_depth, seed=1234, adaptive=True, mode="wavefront", precision="parity",
                tile=None, stripes=None, samples_per_group=0, min_spp=16, rel_threshold=float(np.float32(0.05)),
-               count=False, schedule=None):
+               count=False, schedule=None, generic=False):
         p = RenderParams()
         p.spp, p.max_depth, p.adaptive = spp, max_depth, int(bool(adaptive))
         p.min_spp, p.rel_threshold, p.seed = min_spp, rel_threshold, seed
         p.mode, p.precision = MODES[mode], PRECISIONS[precision]
         p.samples_per_group = samples_per_group
-        p.flags = (1 if count else 0) | {None: 0, "park": 2, "plain": 4}[schedule]
+        p.flags = (1 if count else 0) | SCHEDULE_FLAGS[schedule] | (RTX_FLAG_GENERIC if generic else 0)
         if stripes is not None:
             p.stripe_rows, p.stripe_index, p.stripe_count = stripes
         elif tile is not None:
@@ -320,13 +333,47 @@ class DeviceScene:
                "rtx_encode_p3_device")
         return n.value
 
-    def render_device(self, cam, params, d_rgb, d_spp=0, stream=0):
-        """Device-resident render into caller buffers (e.g. torch tensors' data_ptr())."""
+    def render_device(self, cam, params, d_rgb, d_spp=0, stream=0, stats=True):
+        """Device-resident render into caller buffers (e.g. torch tensors' data_ptr()).
+        stats=False: no statistics, so the call returns without waiting for the render."""
         st = Stats()
         _check(lib().rtx_render_device(self.h, C.byref(cam), C.byref(params), C.c_void_p(d_rgb),
-                                       C.c_void_p(d_spp) if d_spp else None, C.byref(st),
+                                       C.c_void_p(d_spp) if d_spp else None, C.byref(st) if stats else None,
                                        C.c_void_p(stream) if stream else None), "rtx_render_device")
-        return st.as_dict()
+        return st.as_dict() if stats else None
+
+
+def render_multi(scenes, cam, spp, max_depth, seed=1234, adaptive=True, mode="persistent", precision="fast",
+                 stripe_rows=8, stripe_index=0, stripe_count=0, out=None, schedule=None, min_spp=16,
+                 rel_threshold=float(np.float32(0.05))):
+    """One frame over several DeviceScenes (rtx_render_multi): returns the whole-frame
+    (H*W, 3) framebuffer, (H*W,) sample counts, aggregate stats, per-scene stats."""
+    p = RenderParams()
+    p.spp, p.max_depth, p.adaptive = spp, max_depth, int(bool(adaptive))
+    p.min_spp, p.rel_threshold, p.seed = min_spp, rel_threshold, seed
+    p.mode, p.precision = MODES[mode], PRECISIONS[precision]
+    p.flags = SCHEDULE_FLAGS[schedule]
+    p.stripe_rows, p.stripe_index, p.stripe_count = stripe_rows, stripe_index, stripe_count
+    n = len(scenes)
+    npix = cam.image_width * cam.image_height
+    rgb = out if out is not None else np.zeros((npix, 3))
+    sp = np.zeros(npix, np.int32)
+    arr = (C.c_void_p * n)(*[s.h.value for s in scenes])
+    st, per = Stats(), (Stats * n)()
+    _check(lib().rtx_render_multi(arr, n, C.byref(cam), C.byref(p), rgb.ctypes.data_as(C.c_void_p),
+                                  sp.ctypes.data_as(C.c_void_p), C.byref(st), per), "rtx_render_multi")
+    return rgb, sp, st.as_dict(), [x.as_dict() for x in per]
+
+
+def encode_p3(scene, rgb, width, height):
+    """P3 file bytes of a host framebuffer, encoded on `scene`'s device (rtx_encode_p3)."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.float64)
+    cap = lib().rtx_p3_max_bytes(width, height)
+    buf = C.create_string_buffer(cap)
+    n = C.c_size_t()
+    _check(lib().rtx_encode_p3(scene.h, rgb.ctypes.data_as(C.c_void_p), width, height, buf, cap, C.byref(n)),
+           "rtx_encode_p3")
+    return buf.raw[:n.value]
 
 
 def prim_bounds(prims):

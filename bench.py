@@ -1,23 +1,28 @@
 #!/usr/bin/env python3
 """bench.py — Mrays/s of the MI355X path-tracing hot path (BASELINE.json metric).
 
-A "step" is one complete frame of the workload (every sample of every pixel of this rank's
-shard) rendered through the C ABI (rtx_render_device into device-resident buffers, scene
-already in HBM).  Default workload = BASELINE configs[1]: C2 final_scene, 1200x675,
-100 spp, depth 50, fixed spp (adaptive sampling off).
+A "step" is one complete frame: every sample of every pixel of the workload rendered through
+the C ABI (rtx_render_multi: persistent kernel, accumulate, resolve, then the framebuffer
+copied to the host), with the scene already resident in HBM.  The timed region therefore
+runs from the first ray generation to the framebuffer on the host.
 
-N GPUs (one process per GPU, launched by torch.distributed.run): the image's rows are
-split into interleaved 8-row stripes (stripe k -> rank k mod N) and the sample
-count is N x spp, so every rank traces the same amount of work as the 1-GPU run ("weak"
-scaling); no collective touches the data path (RCCL only carries the timing barrier and
-the max-over-ranks reduction).
+Workloads (BASELINE.json configs): the default is the north-star scene, the Stanford bunny:
+  * 1 GPU:  C3, bunny 1000x562, 200 spp, depth 20, fixed spp
+  * N GPUs: C4, bunny 3840x2160, 1024 spp, depth 50, the SAME frame split over the N ranks
+    (strong scaling): the image's rows are interleaved 8-row stripes, stripe k -> rank k mod N
+    (SURVEY §8e); every rank copies its stripes into one shared host framebuffer
+    (/dev/shm); no collective touches the data path (RCCL only carries the timing barrier
+    and the max-over-ranks reduction).
+Other workloads: --workload c2_final | c5_mixed | c1_three | c4_bunny4k | c3_bunny.
 
-Prints ONE JSON line (rank 0).  `roofline` uses the dominant kernel's average launch time
-(HIP events on the library's stream, over the timed region) and the algorithmic bytes per
-launch from a separate counting pass (DESIGN.md "Roofline accounting").  `cpu_baseline`
-times the CPU oracle (oracle/librtx_oracle.so, the restatement pinned to the reference) on
-a bounded crop of the same workload on this host's cores, and `rms_vs_cpu` compares the
-GPU and CPU pixels of that crop at the same seed.
+Prints ONE JSON line (rank 0).  `roofline` prices the dominant kernel (k_persistent) against
+its binding resource, VALU issue: useful lane-operations per second (VALU wave-instructions
+x active lanes, per segment, from the committed rocprofv3 PMC profile of the same build and
+workload) over the MI355X vector peak.  `cpu_baseline` times the CPU restatement of the
+reference (oracle/librtx_oracle.so) on a bounded band of the same frame on this host's
+available cores, with its calibration against the reference itself (profiles/
+cpu_calibration.json, scripts/calibrate_cpu.py), and `rms_vs_cpu` compares that band with
+the GPU's render of it by the same kernel build and schedule the timed frames used.
 """
 import argparse
 import json
@@ -32,23 +37,83 @@ sys.path.insert(0, os.path.join(ROOT, "3360-ray-tracer_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 WORKLOADS = {  # name -> (scene recipe, camera preset, width, spp, depth)
+    "c1_three": ("three", "c1_three", 400, 4, 4),
     "c2_final": ("final", "c2_final", 1200, 100, 50),
     "c3_bunny": ("bunny", "c3_bunny", 1000, 200, 20),
-    "c1_three": ("three", "c1_three", 400, 4, 4),
     "c4_bunny4k": ("bunny", "c4_bunny4k", 3840, 1024, 50),
     "c5_mixed": ("mixed", "c5_mixed", 3840, 2048, 50),
 }
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+CALIBRATION_CASE = {"three": "c1_three", "final": "c2_final", "bunny": "c3_bunny", "mixed": "c5_mixed"}
+# MI355X_MICROARCH.md: 256 CUs x 4 SIMDs, 2400 MHz.  A SIMD retires 16 lanes of a VALU
+# operation per cycle, so a wave64 instruction holds it for 4 cycles (the issue-cost table:
+# v_add_f32 / v_fma_f32 4 cycles; PMC SQ_ACTIVE_INST_VALU counts one quad-cycle per
+# instruction).  Vector peaks: FP64 78.6 TF = 1024 SIMDs x 16 lanes x 2 (FMA) x 2.4 GHz, FP32
+# 157.3 TF with packed FMA.  Non-packed f32 and f64 add / mul / fma issue at this rate.
+N_SIMD, CLOCK_HZ, LANES_PER_CYCLE, CYCLES_PER_VALU = 1024, 2.4e9, 16, 4
+VALU_PEAK_LANE_OPS = N_SIMD * LANES_PER_CYCLE * CLOCK_HZ  # 39.3e12 lane-ops/s
+HBM_PEAK_GBS = 8000.0
 STRIPE_ROWS = 8
+
+
+def available_cpus():
+    """CPUs this process may use: its affinity mask, capped by a cgroup CPU quota."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+class SharedFrame:
+    """The whole-frame host framebuffer: pinned memory (1 rank) or a /dev/shm file every rank
+    maps (N ranks), registered as pinned when the runtime allows it."""
+
+    def __init__(self, torch, npix, rank, world, dist, tag):
+        self.torch, self.path, self.registered = torch, None, False
+        nbytes = npix * 3 * 8
+        if world == 1:
+            self.t = torch.empty((npix, 3), dtype=torch.float64).pin_memory()
+            self.arr = self.t.numpy()
+            self.pinned = True
+            return
+        self.path = f"/dev/shm/rtx_bench_frame_{tag}"
+        if rank == 0:
+            with open(self.path, "wb") as f:
+                f.truncate(nbytes)
+        dist.barrier()
+        self.arr = np.memmap(self.path, dtype=np.float64, mode="r+", shape=(npix, 3))
+        self.pinned = False
+        try:  # plumbing only: lets the library DMA straight into the shared frame
+            rc = torch.cuda.cudart().cudaHostRegister(self.arr.ctypes.data, nbytes, 0)
+            self.registered = self.pinned = int(getattr(rc, "value", rc)) == 0
+        except Exception:  # noqa: BLE001  (pageable: the library stages through pinned memory)
+            self.pinned = False
+
+    def close(self, rank, dist):
+        if self.registered:
+            try:
+                self.torch.cuda.cudart().cudaHostUnregister(self.arr.ctypes.data)
+            except Exception:  # noqa: BLE001
+                pass
+        if self.path:
+            del self.arr
+            if dist is not None:
+                dist.barrier()
+            if rank == 0 and os.path.exists(self.path):
+                os.unlink(self.path)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workload", default="c2_final", choices=sorted(WORKLOADS))
-    ap.add_argument("--spp", type=int, default=0, help="override samples per pixel (per GPU)")
+    ap.add_argument("--steps", type=int, default=0, help="timed frames (0: ~4 s of frames, at least 3)")
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="auto", choices=["auto"] + sorted(WORKLOADS),
+                    help="auto: c3_bunny on 1 GPU, c4_bunny4k split over N GPUs")
+    ap.add_argument("--spp", type=int, default=0, help="override samples per pixel")
     ap.add_argument("--mode", default="persistent", choices=["wavefront", "persistent"])
     ap.add_argument("--precision", default="fast", choices=["parity", "fast"])
     ap.add_argument("--seed", type=int, default=1234)
@@ -56,7 +121,9 @@ def main():
                     help="persistent fast schedule: auto = timed per scene by the library (default); "
                          "plain/park force one (identical results; used by scripts/profile.sh so the "
                          "trace holds no schedule-timing launches)")
+    ap.add_argument("--generic", action="store_true", help="time the generic (unspecialised) kernel build")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-generic-leg", action="store_true", help="skip the generic-build comparison frames")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (=RCCL, one GPU per rank) or gloo (rehearsal)")
     args = ap.parse_args()
@@ -64,7 +131,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    # torch (plumbing: device buffers, barrier, max-over-ranks) must initialise its HIP
+    # torch (plumbing: pinned host memory, barrier, max-over-ranks) must initialise its HIP
     # runtime before librtx.so is loaded into the process
     import torch
 
@@ -80,38 +147,55 @@ def main():
 
     import rtx
 
-    scene_name, preset, width, spp, depth = WORKLOADS[args.workload]
+    workload = args.workload if args.workload != "auto" else ("c3_bunny" if world == 1 else "c4_bunny4k")
+    scene_name, preset, width, spp, depth = WORKLOADS[workload]
     spp = args.spp or spp
-    total_spp = spp * world  # weak scaling: N x samples over 1/N of the pixels
     host = rtx.HostScene.recipe(scene_name, 1234)
     dev = rtx.DeviceScene(host, device=dev_id)
     cam = rtx.camera(rtx.camera_config(preset, width=width))
-    p = rtx.RenderParams()
-    p.spp, p.max_depth, p.adaptive, p.seed = total_spp, depth, 0, args.seed
-    p.mode, p.precision = rtx.MODES[args.mode], rtx.PRECISIONS[args.precision]
-    if world > 1:
+    W, H = cam.image_width, cam.image_height
+    sched_flags = rtx.SCHEDULE_FLAGS[args.schedule] | (rtx.RTX_FLAG_GENERIC if args.generic else 0)
+
+    def params(flags=sched_flags, generic=False):
+        p = rtx.RenderParams()
+        p.spp, p.max_depth, p.adaptive, p.seed = spp, depth, 0, args.seed
+        p.mode, p.precision = rtx.MODES[args.mode], rtx.PRECISIONS[args.precision]
         p.stripe_rows, p.stripe_index, p.stripe_count = STRIPE_ROWS, rank, world
-    sched_flags = {"auto": 0, "park": 2, "plain": 4}[args.schedule]  # RTX_FLAG_PARK / RTX_FLAG_NO_PARK
-    p.flags = sched_flags
-    npix = rtx.lib().rtx_render_pixel_count(cam, p)
+        p.flags = flags | (rtx.RTX_FLAG_GENERIC if generic else 0)
+        return p
 
-    d_rgb = torch.empty((npix, 3), dtype=torch.float64, device=f"cuda:{dev_id}")
-    d_spp = torch.empty((npix,), dtype=torch.int32, device=f"cuda:{dev_id}")
+    frame = SharedFrame(torch, W * H, rank, world, dist, os.environ.get("MASTER_PORT", "0"))
+    if rank == 0:
+        frame.arr[:] = np.nan  # every row must be written by some rank (checked after the run)
+    scenes_arr = (rtx.C.c_void_p * 1)(dev.h.value)
+    out_ptr = frame.arr.ctypes.data
 
-    def step():
-        return dev.render_device(cam, p, d_rgb.data_ptr(), d_spp.data_ptr())
+    def step(p):
+        st = rtx.Stats()
+        rtx._check(rtx.lib().rtx_render_multi(scenes_arr, 1, rtx.C.byref(cam), rtx.C.byref(p), out_ptr, None,
+                                              rtx.C.byref(st), None), "rtx_render_multi")
+        return st.as_dict()
 
     if args.schedule == "auto" and args.mode == "persistent" and args.precision == "fast":
         # the library times its two persistent schedules on the first fast render of a scene
         # (a centre tile at this spp); trigger that here with a one-pixel render, so it never
         # lands in the timed region, whatever --warmup is
         q = rtx.RenderParams()
-        q.spp, q.max_depth, q.adaptive, q.seed, q.mode, q.precision = p.spp, p.max_depth, 0, p.seed, p.mode, p.precision
+        q.spp, q.max_depth, q.adaptive, q.seed, q.mode, q.precision = spp, depth, 0, args.seed, 1, 1
         q.x0, q.y0, q.w, q.h = 0, 0, 1, 1
-        dev.render_device(cam, q, d_rgb.data_ptr(), d_spp.data_ptr())
+        tmp = torch.empty((1, 3), dtype=torch.float64, device=f"cuda:{dev_id}")
+        dev.render_device(cam, q, tmp.data_ptr())
 
-    for _ in range(args.warmup):
-        step()
+    p = params()
+    t_warm = time.perf_counter()
+    for _ in range(max(1, args.warmup)):
+        step(p)
+    per_frame = (time.perf_counter() - t_warm) / max(1, args.warmup)
+    steps = args.steps or max(3, int(4.0 / max(per_frame, 1e-4)))
+    if dist is not None:  # every rank times the same number of frames
+        t = torch.tensor([steps], dtype=torch.int64, device="cpu" if args.dist_backend == "gloo" else f"cuda:{dev_id}")
+        dist.broadcast(t, 0)
+        steps = int(t.item())
 
     def barrier():
         if dist is not None:
@@ -120,12 +204,13 @@ def main():
 
     barrier()
     t0 = time.perf_counter()
-    stats = [step() for _ in range(args.steps)]
+    stats = [step(p) for _ in range(steps)]
     barrier()
     elapsed = time.perf_counter() - t0
     rays = sum(s["rays_total"] for s in stats)
     hot_ms = sum(s["hot_kernel_ms"] for s in stats)
     hot_launches = sum(s["hot_launches"] for s in stats)
+    build_bits, parked = stats[-1]["build"], stats[-1]["parked"]
     if dist is not None:
         red_dev = "cpu" if args.dist_backend == "gloo" else f"cuda:{dev_id}"
         t = torch.tensor([elapsed], dtype=torch.float64, device=red_dev)
@@ -134,43 +219,52 @@ def main():
         r = torch.tensor([rays], dtype=torch.float64, device=red_dev)
         dist.all_reduce(r, op=dist.ReduceOp.SUM)
         rays_all = float(r.item())
+        barrier()
     else:
         rays_all = float(rays)
+    covered = bool(not np.isnan(frame.arr).any()) if rank == 0 else None
 
-    # counting pass (diagnostic kernel build) for algorithmic bytes per segment
-    p.flags = 1 | sched_flags
-    cst = step()
-    p.flags = sched_flags
+    # counting pass (diagnostic kernel build): segments, node visits and SIMD efficiency
+    cst = step(params(rtx.RTX_FLAG_COUNT | sched_flags))
     segs = max(1, cst["rays_total"])
     nodes_per_seg = cst["node_visits"] / segs
-    # SIMD efficiency of the traversal loops (fast BVH4 only): lane work / (64 x wave iterations)
     simd_nodes = cst["node_visits"] / (64.0 * cst["wave_node_iters"]) if cst["wave_node_iters"] else None
     simd_prims = cst["prim_tests"] / (64.0 * cst["wave_prim_iters"]) if cst["wave_prim_iters"] else None
     prims_per_seg = cst["prim_tests"] / segs
-    # B_seg = 32*n_box + 48*n_tri + 16*n_sph + 32*n_rect + 96 (path state in + out).
-    # One box = one 32-B node of the compact model; a visit of the 128-B F4Node tests four boxes,
-    # of the 64-B BVH2 FNode two, of the reference-layout f64 node (parity) one.
     boxes_per_visit = 1 if args.precision == "parity" else cst["node_bytes"] // 32
-    tris_per_seg = cst["tri_tests"] / segs
-    sphs_per_seg = cst["sphere_tests"] / segs
+    tris_per_seg, sphs_per_seg = cst["tri_tests"] / segs, cst["sphere_tests"] / segs
     rects_per_seg = max(0.0, prims_per_seg - tris_per_seg - sphs_per_seg)
+    # SURVEY.md §8(d) byte model: B_seg = 32*n_box + 48*n_tri + 16*n_sph + 32*n_rect + 96.  The
+    # scene is L2/MALL-resident, so these are bytes touched in cache, not HBM traffic.
     bytes_per_seg = (32 * boxes_per_visit * nodes_per_seg + 48 * tris_per_seg + 16 * sphs_per_seg
                      + 32 * rects_per_seg + 96)
     segs_per_launch = rays / max(1, hot_launches)
     avg_launch_s = hot_ms / 1e3 / max(1, hot_launches)
-    achieved_gbs = bytes_per_seg * segs_per_launch / avg_launch_s / 1e9
-    traffic = valu = None
-    tf = os.path.join(ROOT, "profiles", f"traffic_{args.workload}_{args.mode}_{args.precision}.json")
-    if os.path.exists(tf):
-        prof = json.load(open(tf))
-        traffic = prof.get("hbm_bytes_per_launch")
-        if prof.get("valu_busy") is not None:
-            # The kernel's actual limiter is VALU issue (the scene is L2/MALL-resident): the
-            # fraction of SIMD cycles that issue a VALU instruction, from the committed PMC
-            # profile of this build (SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8)).
-            valu = {"busy_frac": prof["valu_busy"], "insts_per_launch": prof.get("valu_insts_per_launch"),
-                    "source": prof.get("source"),
-                    "note": "fraction of SIMD cycles issuing VALU (PMC, profiled run of this build)"}
+
+    roofline = valu_roofline(workload, args, segs_per_launch, avg_launch_s)
+    roofline.update({
+        "kernel": "k_persistent" if args.mode == "persistent" else "k_wf_extend",
+        "avg_launch_ms": avg_launch_s * 1e3, "segments_per_launch": segs_per_launch,
+        "bytes_touched": {"per_segment": bytes_per_seg, "GB_s": bytes_per_seg * segs_per_launch / avg_launch_s / 1e9,
+                          "note": "SURVEY 8(d) algorithmic bytes (nodes/primitives/path state) per segment; "
+                                  "served from L2/MALL (the scene is cache-resident), not an HBM figure"},
+        "nodes_per_segment": nodes_per_seg, "prims_per_segment": prims_per_seg, "boxes_per_visit": boxes_per_visit,
+        "simd_efficiency_nodes": simd_nodes, "simd_efficiency_prims": simd_prims,
+    })
+
+    generic_leg = None
+    if world == 1 and not args.generic and not args.no_generic_leg and args.mode == "persistent":
+        gp = params(generic=True)
+        step(gp)
+        g_steps = max(3, min(steps, int(1.5 / max(per_frame, 1e-4))))
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        gst = [step(gp) for _ in range(g_steps)]
+        torch.cuda.synchronize()
+        tg = time.perf_counter() - tg
+        generic_leg = {"value": sum(s["rays_total"] for s in gst) / tg / 1e6, "ms_per_step": tg * 1e3 / g_steps,
+                       "steps": g_steps, "build": rtx.build_names(gst[-1]["build"]),
+                       "note": "same frame with RTX_FLAG_GENERIC: no per-scene specialisation (same pixels)"}
 
     out = None
     if rank == 0:
@@ -179,36 +273,32 @@ def main():
             "value": rays_all / elapsed / 1e6,
             "unit": "Mrays/s",
             "n_gpus": world,
-            "steps": args.steps,
+            "steps": steps,
             "warmup": args.warmup,
-            "ms_per_step": elapsed * 1e3 / args.steps,
+            "ms_per_step": elapsed * 1e3 / steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": f"{args.workload}: {scene_name} scene {width}x{cam.image_height}, "
-                                   f"{spp} spp/GPU-share, depth {depth}, fixed spp",
+            "config": {"workload": f"{workload}: {scene_name} scene {W}x{H}, {spp} spp, depth {depth}, fixed spp"
+                                   + (f", one frame split over {world} GPUs" if world > 1 else ""),
                        "scene_prims": int(host.desc().n_prims), "bvh_nodes": int(host.desc().n_nodes),
-                       "mode": args.mode, "precision": args.precision, "spp_total": total_spp,
-                       "pixels_per_rank": int(npix), "stripe_rows": STRIPE_ROWS if world > 1 else None,
-                       "schedule": "park" if stats[-1].get("parked") else "plain",
-                       "parallelism": f"tile-split x{world} (interleaved row stripes, no collectives)"},
-            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_persistent" if args.mode == "persistent" else "k_wf_bounce",
-                         "avg_launch_ms": avg_launch_s * 1e3, "segments_per_launch": segs_per_launch,
-                         "bytes_per_segment": bytes_per_seg, "nodes_per_segment": nodes_per_seg,
-                         "prims_per_segment": prims_per_seg, "tris_per_segment": tris_per_seg,
-                         "spheres_per_segment": sphs_per_seg, "boxes_per_visit": boxes_per_visit,
-                         "simd_efficiency_nodes": simd_nodes, "simd_efficiency_prims": simd_prims,
-                         "valu": valu,
-                         "note": "algorithmic bytes per SURVEY 8(d); the scene is L2/MALL-resident, so "
-                                 "HBM traffic (PMC) << algorithmic bytes and frac may exceed 1"},
-            "rays_per_step": rays_all / args.steps,
+                       "mode": args.mode, "precision": args.precision,
+                       "schedule": "park" if parked else "plain", "kernel_build": rtx.build_names(build_bits),
+                       "timed_region": "first ray generation -> framebuffer on the host (D2H inside each step)",
+                       "framebuffer": "pinned host" if frame.pinned else "pageable host (pinned staging)",
+                       "frame_rows_covered": covered,
+                       "parallelism": f"tile-split x{world} (interleaved {STRIPE_ROWS}-row stripes, no collectives)"},
+            "roofline": roofline,
+            "rays_per_step": rays_all / steps,
         }
+        if generic_leg:
+            out["generic_build"] = generic_leg
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"], out["rms_vs_cpu"] = cpu_baseline(rtx, dev, host, cam, preset, spp, depth, args)
+            out["cpu_baseline"], out["rms_vs_cpu"], out["rms_check"] = cpu_baseline(
+                rtx, dev, host, cam, preset, scene_name, spp, depth, args, parked, build_bits)
+    frame.close(rank, dist)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
@@ -216,43 +306,90 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(rtx, dev, host, cam, preset, spp, depth, args):
-    """Time the CPU oracle on a centred crop of the same workload; compare its pixels."""
+def valu_roofline(workload, args, segs_per_launch, avg_launch_s):
+    """VALU-issue roofline of the hot kernel from the committed PMC profile of this build.
+
+    useful lane-ops / segment = SQ_INSTS_VALU x 64 x lane utilisation / segments, where lane
+    utilisation = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU) (PMC, same launch); achieved =
+    that x segments per launch (this run) / average launch time (this run, HIP events)."""
+    pf = os.path.join(ROOT, "profiles", f"valu_{workload}_{args.mode}_{args.precision}.json")
+    base = {"bound": "valu", "peak": VALU_PEAK_LANE_OPS / 1e12, "unit": "Tlane-op/s (VALU)"}
+    if not os.path.exists(pf):
+        return {**base, "achieved": None, "frac": None, "traffic": None, "note": f"no PMC profile {pf}"}
+    prof = json.load(open(pf))
+    ops_per_seg = prof["lane_ops_per_segment"]
+    insts_per_seg = prof["valu_insts_per_segment"]
+    achieved = ops_per_seg * segs_per_launch / avg_launch_s
+    issue = insts_per_seg * segs_per_launch * CYCLES_PER_VALU / avg_launch_s / (N_SIMD * CLOCK_HZ)
+    traffic = prof.get("hbm_bytes_per_segment")
+    return {**base, "achieved": achieved / 1e12, "frac": achieved / VALU_PEAK_LANE_OPS,
+            "traffic": traffic * segs_per_launch if traffic is not None else None,
+            "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, scaled to this launch)",
+            "hbm_GB_s": traffic * segs_per_launch / avg_launch_s / 1e9 if traffic is not None else None,
+            "hbm_frac": (traffic * segs_per_launch / avg_launch_s / 1e9 / HBM_PEAK_GBS) if traffic is not None else None,
+            "valu_issue_frac": issue, "lane_utilisation": prof["lane_utilisation"],
+            "lane_ops_per_segment": ops_per_seg, "valu_insts_per_segment": insts_per_seg,
+            "source": prof["source"],
+            "note": "VALU lane-ops: a wave64 VALU instruction holds a SIMD for 4 cycles (16 lanes/cycle); "
+                    "frac = useful (active-lane) operations / (1024 SIMDs x 16 lanes x 2.4 GHz); "
+                    "valu_issue_frac = issue cycles used incl. idle lanes / SIMD cycles"}
+
+
+def cpu_baseline(rtx, dev, host, cam, preset, scene_name, spp, depth, args, parked, build_bits):
+    """Time the CPU oracle on a centred band of the same frame; compare its pixels with the
+    GPU's render of the band by the timed kernel build and schedule."""
     import tempfile
 
     import oracle_ctypes as orc
 
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    threads = args.cpu_threads or available_cpus()
     W, H = cam.image_width, cam.image_height
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "scene.rtxs")
         host.write(path)
         s = orc.Scene(path)
         cfg = orc.camera_preset(preset)
-        # probe on a small centre crop (twice: the first call also starts the thread pool),
-        # then size the timed sample to ~10 s of wall time on `threads` cores, capped at the
-        # whole frame: full-width bands of rows around the image centre
-        probe = (0, H // 2 - 4, W, 8)
+        # probe on a small centre band (twice: the first call also starts the thread pool),
+        # then size the timed sample to ~15 s of wall time, capped at the whole frame
+        probe = (0, H // 2 - 2, W, 4)
         for _ in range(2):
             t0 = time.perf_counter()
             s.render(cfg, W, spp, depth, args.seed, adaptive=0, rng="philox", mode="per_pixel", tile=probe,
                      threads=threads)
-            per_row = (time.perf_counter() - t0) / 8
-        ch = int(max(8, min(H, 10.0 / max(per_row, 1e-6))))
-        cw = W
-        tile = (0, max(0, H // 2 - ch // 2), cw, ch)
+            per_row = (time.perf_counter() - t0) / 4
+        ch = int(max(4, min(H, 15.0 / max(per_row, 1e-6))))
+        tile = (0, max(0, H // 2 - ch // 2), W, ch)
         t0 = time.perf_counter()
         ref, _, st = s.render(cfg, W, spp, depth, args.seed, adaptive=0, rng="philox", mode="per_pixel", tile=tile,
                               threads=threads)
         dt = time.perf_counter() - t0
-    gpu, _, _ = dev.render(cam, spp, depth, seed=args.seed, adaptive=False, tile=tile, mode="wavefront",
-                           precision="parity")
+    sched = "park" if parked else "plain"
+    gpu, _, gst = dev.render(cam, spp, depth, seed=args.seed, adaptive=False, tile=tile, mode=args.mode,
+                             precision=args.precision, schedule=sched if args.mode == "persistent" else None,
+                             generic=args.generic)
     rms = float(np.sqrt(np.mean((gpu - ref.reshape(-1, 3)) ** 2)))
-    what = "the whole" if ch == H else f"centre band {cw}x{ch} of the same"
-    base = {"value": st["rays"] / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+    what = "the whole" if ch == H else f"centre band {W}x{ch} of the same"
+    base = {"value": st["rays"] / dt / 1e6, "unit": "Mrays/s", "cores": threads, "nproc": os.cpu_count(),
+            "kind": "port",
             "sample": f"{what} {W}x{H} frame, {spp} spp, depth {depth}, fixed spp, "
-                      f"{st['rays']} segments in {dt:.1f}s (oracle/rtx_oracle.cc, OpenMP, philox)"}
-    return base, rms
+                      f"{st['rays']} segments in {dt:.1f}s (oracle/rtx_oracle.cc, OpenMP on {threads} threads, philox)"}
+    cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+    if os.path.exists(cal):
+        c = json.load(open(cal))
+        case = c["cases"].get(CALIBRATION_CASE.get(scene_name, ""))
+        if case:
+            r = case["ratio_port_over_reference"]
+            base["calibration"] = {
+                "ratio_port_over_reference": r, "case": case["config"], "threads": c["threads"],
+                "where": c["host"], "reference_mrays_s": case["reference"]["mrays_s"],
+                "port_mrays_s": case["port"]["mrays_s"],
+                "reference_equivalent_value": base["value"] / r,
+                "note": "port and reference (its own sources, oracle/_ref) timed on identical configs and threads; "
+                        "reference_equivalent_value = value / ratio estimates the reference on these cores"}
+    check = {"mode": args.mode, "precision": args.precision, "schedule": sched,
+             "kernel_build": rtx.build_names(gst["build"]), "same_build_as_timed": gst["build"] == build_bits,
+             "rows": [tile[1], tile[1] + tile[3]]}
+    return base, rms, check
 
 
 if __name__ == "__main__":

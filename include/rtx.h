@@ -41,7 +41,8 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 3  /* 2: rtx_stats.node_bytes; 3: rtx_stats.parked, RTX_FLAG_PARK / NO_PARK */
+#define RTX_ABI_VERSION 4  /* 2: rtx_stats.node_bytes; 3: rtx_stats.parked, RTX_FLAG_PARK / NO_PARK;
+                              4: rtx_stats.build, RTX_FLAG_GENERIC, rtx_render_multi */
 
 enum {
   RTX_OK = 0,
@@ -199,7 +200,24 @@ enum {
      default the first such render of a scene times both on a centre tile and keeps the
      faster for the scene; these flags force one */
   RTX_FLAG_PARK = 2,   /* park long traversals and resume them in the next segment round */
-  RTX_FLAG_NO_PARK = 4 /* every traversal runs to completion within its round */
+  RTX_FLAG_NO_PARK = 4, /* every traversal runs to completion within its round */
+  /* RTX_MODE_PERSISTENT: run the generic kernel build, without the per-scene
+     specialisations (same results; for measuring what the specialisations buy) */
+  RTX_FLAG_GENERIC = 8
+};
+
+/* rtx_stats.build: which persistent-kernel build ran (the per-scene specialisations compile
+   out code paths the scene cannot reach; every build gives identical results) */
+enum {
+  RTX_BUILD_PARK = 1,           /* parked-traversal schedule */
+  RTX_BUILD_SPHERE_TREE = 2,    /* leaf tests for spheres only (every tree primitive a sphere) */
+  RTX_BUILD_TRIANGLE_TREE = 4,  /* leaf tests for triangles only */
+  RTX_BUILD_LAMBERTIAN = 8,     /* shading for Lambertian materials only */
+  RTX_BUILD_NO_TEXTURES = 16,   /* no texture lookups (every colour in the material table) */
+  RTX_BUILD_NO_DEFOCUS = 32,    /* no thin-lens camera sampling (defocus_angle <= 0) */
+  RTX_BUILD_FAST = 64,          /* RTX_PREC_FAST traversal */
+  RTX_BUILD_COUNT = 128,        /* diagnostic counting build */
+  RTX_BUILD_SCATTER = 256       /* MegaKernel (Scatter API) semantics */
 };
 
 typedef struct {
@@ -217,6 +235,7 @@ typedef struct {
   uint64_t tri_tests;       /* with RTX_FLAG_COUNT: triangle / sphere tests among prim_tests (rest: rects) */
   uint64_t sphere_tests;
   uint64_t parked;          /* 1: the persistent fast schedule that parks long traversals ran */
+  uint64_t build;           /* RTX_BUILD_* bits of the persistent kernel build (0: wavefront mode) */
 } rtx_stats;
 
 /* ---- entry points ------------------------------------------------------------------ */
@@ -247,6 +266,21 @@ int64_t rtx_render_pixel_count(const rtx_camera* cam, const rtx_render_params* p
 /* Device-resident variant: out buffers are device pointers; asynchronous on stream. */
 int rtx_render_device(rtx_scene* scene, const rtx_camera* cam, const rtx_render_params* params,
                       double* d_out_rgb, int32_t* d_out_spp, rtx_stats* stats, void* stream);
+
+/* One frame over several devices: the image's rows are split into interleaved
+ * stripes of params->stripe_rows rows (0: 8), and scenes[k] renders stripe
+ * params->stripe_index + k of params->stripe_count (stripe_count <= 0: n stripes, from 0), each
+ * from its own host thread on its scene's stream.  The stripes come back to the host and are
+ * placed at their rows of out_rgb (W x H x 3, the whole frame; a pinned buffer receives them by
+ * DMA, a pageable one through pinned staging) and out_spp (W x H, may be NULL); rows of other
+ * stripes are not written, so several processes may fill one shared framebuffer.  Replaces
+ * WavefrontRenderer::Render()'s one framebuffer (renderer/wavefront.cc:228-241) for G GPUs.
+ * One scene per device is the intended use (rtx_scene_create on each; the same description);
+ * a scene may not appear twice.  The RNG is keyed by the global pixel, so the image is
+ * bit-identical for every n and split.  stats: counters summed, times = max over scenes;
+ * per_scene (n entries) may be NULL. */
+int rtx_render_multi(rtx_scene* const* scenes, int32_t n, const rtx_camera* cam, const rtx_render_params* params,
+                     double* out_rgb, int32_t* out_spp, rtx_stats* stats, rtx_stats* per_scene);
 
 /* ---- host-side scene assembly (C++ host library, no GPU) --------------------------- */
 
@@ -292,6 +326,12 @@ int rtx_render_p3(rtx_scene* scene, const rtx_camera* cam, const rtx_render_para
    device buffer d_out (cap >= rtx_p3_max_bytes); synchronizes `stream` to report *out_len. */
 int rtx_encode_p3_device(rtx_scene* scene, const double* d_rgb, int32_t width, int32_t height, char* d_out,
                          size_t cap, size_t* out_len, void* stream);
+
+/* P3 file bytes of a host linear framebuffer (width x height x 3 doubles), encoded on the
+   scene's device (e.g. the gathered frame of rtx_render_multi); out: host, cap >=
+   rtx_p3_max_bytes. */
+int rtx_encode_p3(rtx_scene* scene, const double* rgb, int32_t width, int32_t height, char* out, size_t cap,
+                  size_t* out_len);
 
 /* write_color bytes (core/color.h:18-33) as a P3 PPM; rgb is a linear framebuffer (host). */
 int rtx_write_ppm(const char* path, const double* rgb, int32_t width, int32_t height);

@@ -42,6 +42,7 @@
 
 #include <omp.h>
 
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -489,6 +490,7 @@ void render_wavefront(RefScene& S, Cam& cam, int max_depth, int max_spp, int bat
     integrator::RecordSample(ps, L);
     if (!ps.converged && integrator::IsConverged(ps, kRelThresh, kMinSamples)) ps.converged = true;
   };
+  const auto t_start = std::chrono::steady_clock::now();
   for (int s = 0; s < max_spp; ++s) {
     q.clear();
     for (int y = 0; y < H; ++y)
@@ -568,6 +570,7 @@ void render_wavefront(RefScene& S, Cam& cam, int max_depth, int max_spp, int bat
       nq.clear();
     }
   }
+  const auto t_loop = std::chrono::steady_clock::now();
   std::vector<double> fb(3 * (size_t)N);
   std::vector<int> spp(N);
   std::ofstream ppm(out + ".ppm");
@@ -582,8 +585,15 @@ void render_wavefront(RefScene& S, Cam& cam, int max_depth, int max_spp, int bat
   }
   write_bin(out + ".f64", fb);
   write_bin(out + ".spp", spp);
+  ppm.close();
+  const auto t_end = std::chrono::steady_clock::now();
   std::ofstream st(out + ".stats");
   st << "rays " << rays << "\nprimaries " << primaries << "\n";
+  // wall seconds of the pass loop (generation .. shading) and of the whole Render()
+  // including the P3 write (the reference's `Runtime:` covers the latter, main.cc:196)
+  st << "loop_seconds " << std::chrono::duration<double>(t_loop - t_start).count() << "\n";
+  st << "render_seconds " << std::chrono::duration<double>(t_end - t_start).count() << "\n";
+  st << "threads " << omp_get_max_threads() << "\n";
 }
 
 // Megakernel mode (mega_kernel.h:15-54 + DefaultSampler sampler.h:22-34 + GetPixel
@@ -705,7 +715,11 @@ Cam parse_cam(char** a) {
 }  // namespace
 
 int main(int argc, char** argv) {
-  omp_set_num_threads(1);
+  // Single-threaded by default (bit-reproducible under SeedRng).  REF_THREADS=n runs the
+  // reference's OpenMP IntersectBatch on n threads (the CPU-rate calibration): its shading
+  // loop stays on the main thread, so the result is the same.
+  const char* nt = std::getenv("REF_THREADS");
+  omp_set_num_threads(nt ? std::max(1, std::atoi(nt)) : 1);
   if (argc < 2) usage();
   std::string cmd = argv[1];
   if (cmd == "recipe" && argc == 4) {

@@ -1,10 +1,11 @@
 #!/bin/bash
 # One GPU session: parity tests, then benches.  Stops at the first abnormal exit
 # (fault / abort / timeout); ordinary test failures (pytest rc 1) do not stop the benches.
+#   scripts/gpu_round.sh <tag> ["<bench args>" ...]
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 mkdir -p gpurun_out
 TAG=${1:-run}
-timeout -k 10 600 python -m pytest tests -m gpu -q --timeout 300 -rf > gpurun_out/pytest_gpu_$TAG.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -rf > gpurun_out/pytest_gpu_$TAG.log 2>&1
 rc=$?
 echo "pytest exit $rc" >> gpurun_out/pytest_gpu_$TAG.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi

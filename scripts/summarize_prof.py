@@ -71,6 +71,42 @@ def main():
             json.dump(t, open(os.path.join(ROOT, "profiles", f"traffic_{workload}_{mode}_{prec}.json"), "w"),
                       indent=1)
             print(json.dumps(t))
+            valu_profile(d, k, v, launches, per, rnd, tag, workload, mode, prec)
+
+
+def per_launch(v, launches, k, c):
+    return v[c] / max(1, len(launches[(k, c)]))
+
+
+def valu_profile(d, k, v, launches, hbm_per_launch, rnd, tag, workload, mode, prec):
+    """profiles/valu_<workload>_<mode>_<precision>.json: what bench.py's VALU roofline reads.
+    Segments per launch come from the bench line of the PMC pass (the frames are identical)."""
+    need = ("SQ_INSTS_VALU", "SQ_ACTIVE_INST_VALU", "SQ_THREAD_CYCLES_VALU")
+    if not all(c in v for c in need):
+        return
+    b = glob.glob(os.path.join(d, "bench_pmc_SQ_INSTS_VALU*.json"))
+    segs = json.loads(open(b[0]).read().strip().splitlines()[-1])["roofline"]["segments_per_launch"]
+    insts = per_launch(v, launches, k, "SQ_INSTS_VALU")
+    active = per_launch(v, launches, k, "SQ_ACTIVE_INST_VALU")
+    threads = per_launch(v, launches, k, "SQ_THREAD_CYCLES_VALU")
+    # SQ_THREAD_CYCLES_VALU counts SQ_ACTIVE_INST_VALU's cycles x active lanes (same unit):
+    # the ratio over 64 is the mean fraction of a wave's lanes that VALU instructions use
+    util = threads / (64.0 * active)
+    out = {"kernel": k, "segments_per_launch": segs, "valu_insts_per_launch": insts,
+           "active_inst_valu_per_launch": active, "thread_cycles_valu_per_launch": threads,
+           "lane_utilisation": util, "valu_insts_per_segment": insts / segs,
+           "lane_ops_per_segment": insts * 64 * util / segs,
+           "hbm_bytes_per_segment": hbm_per_launch / segs,
+           "source": f"profiles/{rnd}/pmc_{tag}.json",
+           "formula": "lane_ops_per_segment = SQ_INSTS_VALU x 64 x SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU)"
+                      " / segments; hbm = (FETCH_SIZE x 2 + WRITE_SIZE) x 1 KiB / segments"}
+    for c in ("GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+              "SQ_ACTIVE_INST_ANY", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_LDS",
+              "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"):
+        if c in v:
+            out[c.lower() + "_per_launch"] = per_launch(v, launches, k, c)
+    json.dump(out, open(os.path.join(ROOT, "profiles", f"valu_{workload}_{mode}_{prec}.json"), "w"), indent=1)
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":

@@ -1,0 +1,271 @@
+"""GPU parity of the code the benchmark times, and of the multi-device frame.
+
+The persistent fast kernel comes in per-scene builds (rtx_stats.build: sphere/triangle leaf
+tests, Lambertian-only shading, no texture lookups, no thin-lens sampling, PARK schedule).
+Every build the BASELINE configurations select is compared here with the CPU oracle at the
+same Philox seed, on crops of the configurations' own cameras and image sizes:
+  * C2 final_scene 1200x675 depth 50 (sphere tree, no textures, no defocus; plain)
+  * C3/C4 bunny 1000x562 depth 20 / 3840x2160 depth 50 (triangle tree, Lambertian, no
+    textures; PARK)
+  * C5 mixed 3840x2160 depth 50 (sphere tree, textures, all three BSDFs; plain and PARK)
+  * thin-lens cameras (defocusAngle > 0: the builds with camera disk sampling), every mode
+and the generic build must give the same pixels as the specialised ones, bit for bit.
+
+Tolerance: RMS <= 1e-4 on the linear framebuffer; with fixed spp the segment
+counts are identical.  Multi-device frames (rtx_render_multi) must be bit-identical to the
+single-device frame, however many scenes share the work.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import scene_path
+
+pytestmark = pytest.mark.gpu
+RMS_TOL = 1e-4
+THREADS = min(16, os.cpu_count() or 1)
+
+
+@pytest.fixture(scope="module")
+def scenes(rtx_mod, gpu, mixed_scene_file):
+    cache = {}
+
+    def get(name):
+        if name not in cache:
+            path = mixed_scene_file if name == "mixed" else scene_path(name)
+            cache[name] = (path, rtx_mod.DeviceScene(rtx_mod.HostScene.load(path)))
+        return cache[name]
+
+    return get
+
+
+def oracle(orc, path, preset, width, spp, depth, seed, tile, adaptive=0, mode="per_pixel", **cam):
+    cfg = orc.camera_preset(preset, **cam)
+    return orc.Scene(path).render(cfg, width, spp, depth, seed, adaptive=adaptive, rng="philox", mode=mode,
+                                  tile=tile, threads=THREADS)
+
+
+def centre_tile(cam, w, h, dx=0, dy=0):
+    return ((cam.image_width - w) // 2 + dx, (cam.image_height - h) // 2 + dy, w, h)
+
+
+# scene, preset, full width, spp, depth, build of the plain / the PARK schedule
+SPH = {"sphere_tree", "no_textures", "no_defocus"}
+TRI = {"triangle_tree", "lambertian", "no_textures", "park"}
+BENCH_CASES = [
+    ("final", "c2_final", 1200, 8, 50, SPH, {"park"}),
+    ("bunny", "c3_bunny", 1000, 6, 20, set(), TRI),
+    ("bunny", "c4_bunny4k", 3840, 4, 50, set(), TRI),
+    ("mixed", "c5_mixed", 3840, 4, 50, {"sphere_tree"}, {"park"}),
+]
+SPECIALISED = {"sphere_tree", "triangle_tree", "lambertian", "no_textures", "no_defocus", "park"}
+
+
+@pytest.mark.parametrize("schedule", ["plain", "park", "auto"])
+@pytest.mark.parametrize("case", BENCH_CASES, ids=[c[1] for c in BENCH_CASES])
+def test_timed_kernel_builds_match_oracle(rtx_mod, orc, scenes, case, schedule):
+    scene, preset, width, spp, depth, plain_build, park_build = case
+    path, d = scenes(scene)
+    cam = rtx_mod.camera(rtx_mod.camera_config(preset, width=width))
+    tile = centre_tile(cam, 40, 24)
+    ref, _, ref_st = oracle(orc, path, preset, width, spp, depth, 77, tile)
+    rgb, sp, st = d.render(cam, spp, depth, seed=77, adaptive=False, mode="persistent", precision="fast", tile=tile,
+                           schedule=schedule)
+    names = set(rtx_mod.build_names(st["build"])) & SPECIALISED
+    want = {"plain": plain_build, "park": park_build}.get(schedule) or (park_build if st["parked"] else plain_build)
+    assert names == want, (names, want)
+    rms = np.sqrt(np.mean((rgb - ref.reshape(-1, 3)) ** 2))
+    assert rms <= RMS_TOL, rms
+    assert np.all(sp == spp) and st["rays_total"] == ref_st["rays"]
+
+
+@pytest.mark.parametrize("case", BENCH_CASES, ids=[c[1] for c in BENCH_CASES])
+def test_generic_build_equals_specialised(rtx_mod, scenes, case):
+    """Specialisation compiles out unreachable code only: identical pixels and counts."""
+    scene, preset, width, spp, depth, _, _ = case
+    _, d = scenes(scene)
+    cam = rtx_mod.camera(rtx_mod.camera_config(preset, width=width))
+    tile = centre_tile(cam, 64, 32, dy=5)
+    a, sa, sta = d.render(cam, spp, depth, seed=3, adaptive=False, mode="persistent", precision="fast", tile=tile)
+    b, sb, stb = d.render(cam, spp, depth, seed=3, adaptive=False, mode="persistent", precision="fast", tile=tile,
+                          generic=True)
+    spec = set(rtx_mod.build_names(stb["build"])) & (SPECIALISED - {"park"})
+    assert not spec, spec
+    assert sta["parked"] == stb["parked"]  # the generic flag keeps the scene's schedule
+    assert np.array_equal(a, b) and np.array_equal(sa, sb) and sta["rays_total"] == stb["rays_total"]
+
+
+def test_c4_full_width_rows_match_oracle(rtx_mod, orc, scenes):
+    """C4 (bunny 3840x2160, depth 50): two full-width row bands, far apart, on the timed
+    kernel (automatic schedule), against the oracle."""
+    path, d = scenes("bunny")
+    cam = rtx_mod.camera(rtx_mod.camera_config("c4_bunny4k", width=3840))
+    assert (cam.image_width, cam.image_height) == (3840, 2160)
+    for y0 in (1000, 1700):
+        tile = (0, y0, 3840, 2)
+        ref, _, ref_st = oracle(orc, path, "c4_bunny4k", 3840, 2, 50, 4096, tile)
+        rgb, _, st = d.render(cam, 2, 50, seed=4096, adaptive=False, mode="persistent", precision="fast", tile=tile)
+        rms = np.sqrt(np.mean((rgb - ref.reshape(-1, 3)) ** 2))
+        assert rms <= RMS_TOL, (y0, rms)
+        assert st["rays_total"] == ref_st["rays"]
+
+
+DOF = {"defocusAngle": 0.6, "focusDist": 10.0}
+DOF_CASES = [  # scene, preset, width, spp, depth, adaptive
+    ("final", "c2_final", 48, 6, 50, 1),
+    ("bunny", "c3_bunny", 40, 4, 20, 0),
+    ("mixed", "c5_mixed", 40, 4, 50, 0),
+    ("cornell", "cornell", 30, 8, 20, 1),
+]
+
+
+@pytest.mark.parametrize("precision", ["parity", "fast"])
+@pytest.mark.parametrize("mode", ["wavefront", "persistent"])
+@pytest.mark.parametrize("case", DOF_CASES, ids=[c[0] for c in DOF_CASES])
+def test_defocus_camera_matches_oracle(rtx_mod, orc, scenes, case, mode, precision):
+    """Thin-lens cameras (camera.h:134-144 defocus_disk_sample, math_utils.h:83-88
+    RandomInUnitDisk rejection loop): the builds that keep camera disk sampling."""
+    scene, preset, w, spp, depth, adaptive = case
+    path, d = scenes(scene)
+    ref, ref_spp, ref_st = oracle(orc, path, preset, w, spp, depth, 606, None, adaptive=adaptive, **DOF)
+    cam = rtx_mod.camera(rtx_mod.camera_config(preset, width=w, defocus=DOF["defocusAngle"], focus=DOF["focusDist"]))
+    assert cam.defocus_angle > 0
+    scheds = ["plain", "park"] if (mode, precision) == ("persistent", "fast") else [None]
+    for sched in scheds:
+        rgb, sp, st = d.render(cam, spp, depth, seed=606, adaptive=adaptive, mode=mode, precision=precision,
+                               schedule=sched)
+        assert "no_defocus" not in rtx_mod.build_names(st["build"])
+        rms = np.sqrt(np.mean((rgb - ref.reshape(-1, 3)) ** 2))
+        assert rms <= RMS_TOL, (sched, rms)
+        assert np.array_equal(sp, ref_spp.ravel())
+        if not adaptive:
+            assert st["rays_total"] == ref_st["rays"]
+        if precision == "parity":
+            assert np.all(rgb == ref.reshape(-1, 3), 1).mean() >= 0.95
+
+
+def test_defocus_megakernel_matches_oracle(rtx_mod, orc, scenes):
+    path, d = scenes("final")
+    ref, _, ref_st = oracle(orc, path, "c2_final", 32, 3, 50, 91, None, mode="megakernel", **DOF)
+    cam = rtx_mod.camera(rtx_mod.camera_config("c2_final", width=32, defocus=0.6, focus=10.0))
+    for precision in ("parity", "fast"):
+        rgb, _, st = d.render(cam, 3, 50, seed=91, adaptive=False, mode="megakernel", precision=precision)
+        assert np.sqrt(np.mean((rgb - ref.reshape(-1, 3)) ** 2)) <= RMS_TOL
+        assert st["rays_total"] == ref_st["rays"]
+
+
+def test_defocus_changes_the_image(rtx_mod, scenes):
+    """Guard: the thin-lens path is really taken (a pinhole render differs)."""
+    _, d = scenes("final")
+    cam0 = rtx_mod.camera(rtx_mod.camera_config("c2_final", width=48))
+    cam1 = rtx_mod.camera(rtx_mod.camera_config("c2_final", width=48, defocus=0.6, focus=10.0))
+    a, _, _ = d.render(cam0, 4, 50, seed=1, adaptive=False, mode="persistent", precision="fast")
+    b, _, _ = d.render(cam1, 4, 50, seed=1, adaptive=False, mode="persistent", precision="fast")
+    assert not np.array_equal(a, b)
+
+
+# ---- multi-device frame (rtx_render_multi) -------------------------------------------------
+
+def test_render_multi_same_device_twice_is_bit_identical(rtx_mod, scenes):
+    """Two (and three) scenes on device 0, each with its own host thread and stream, split
+    the frame into interleaved stripes; the gathered frame equals the one-device frame."""
+    path, d = scenes("final")
+    cam = rtx_mod.camera(rtx_mod.camera_config("c2_final", width=96))
+    full, fsp, fst = d.render(cam, 5, 50, seed=12, adaptive=False, mode="persistent", precision="fast")
+    extra = [rtx_mod.DeviceScene(rtx_mod.HostScene.load(path)) for _ in range(2)]
+    for group in ([d, extra[0]], [d, extra[0], extra[1]]):
+        for rows in (8, 3):
+            rgb, sp, st, per = rtx_mod.render_multi(group, cam, 5, 50, seed=12, adaptive=False, stripe_rows=rows)
+            assert np.array_equal(rgb, full) and np.array_equal(sp, fsp), (len(group), rows)
+            assert st["rays_total"] == fst["rays_total"] and sum(p["rays_total"] for p in per) == st["rays_total"]
+            assert all(p["rays_total"] > 0 for p in per)
+
+
+def test_render_multi_adaptive_and_parity(rtx_mod, scenes):
+    path, d = scenes("cornell")
+    cam = rtx_mod.camera(rtx_mod.camera_config("cornell", width=40))
+    other = rtx_mod.DeviceScene(rtx_mod.HostScene.load(path))
+    full, fsp, _ = d.render(cam, 24, 20, seed=5, adaptive=True, mode="wavefront", precision="parity")
+    rgb, sp, _, _ = rtx_mod.render_multi([d, other], cam, 24, 20, seed=5, adaptive=True, mode="wavefront",
+                                         precision="parity")
+    assert np.array_equal(rgb, full) and np.array_equal(sp, fsp)
+
+
+def test_render_multi_partial_stripes_write_only_their_rows(rtx_mod, scenes):
+    """A process that owns stripes 1 and 2 of 4 writes exactly those rows of the shared
+    frame (the bench's multi-process gather)."""
+    path, d = scenes("final")
+    cam = rtx_mod.camera(rtx_mod.camera_config("c2_final", width=64))
+    H, W = cam.image_height, cam.image_width
+    full, _, _ = d.render(cam, 3, 50, seed=8, adaptive=False, mode="persistent", precision="fast")
+    other = rtx_mod.DeviceScene(rtx_mod.HostScene.load(path))
+    sentinel = -7.0
+    out = np.full((H * W, 3), sentinel)
+    rtx_mod.render_multi([d, other], cam, 3, 50, seed=8, adaptive=False, stripe_rows=4, stripe_index=1,
+                         stripe_count=4, out=out)
+    mine = set(rtx_mod.stripe_rows_of(H, 4, 1, 4)) | set(rtx_mod.stripe_rows_of(H, 4, 2, 4))
+    o, f = out.reshape(H, W, 3), full.reshape(H, W, 3)
+    for y in range(H):
+        if y in mine:
+            assert np.array_equal(o[y], f[y]), y
+        else:
+            assert np.all(o[y] == sentinel), y
+
+
+def test_render_multi_into_pinned_buffer(rtx_mod, scenes):
+    """A pinned caller framebuffer receives the stripes by strided DMA: same bytes."""
+    import torch
+
+    path, d = scenes("final")
+    cam = rtx_mod.camera(rtx_mod.camera_config("c2_final", width=80))
+    full, _, _ = d.render(cam, 2, 50, seed=4, adaptive=False, mode="persistent", precision="fast")
+    other = rtx_mod.DeviceScene(rtx_mod.HostScene.load(path))
+    pinned = torch.zeros((cam.image_width * cam.image_height, 3), dtype=torch.float64).pin_memory()
+    out = pinned.numpy()
+    rtx_mod.render_multi([d, other], cam, 2, 50, seed=4, adaptive=False, out=out)
+    assert np.array_equal(out, full)
+
+
+def test_render_multi_rejects_bad_arguments(rtx_mod, scenes):
+    _, d = scenes("final")
+    cam = rtx_mod.camera(rtx_mod.camera_config("c2_final", width=16))
+    with pytest.raises(rtx_mod.RtxError, match="twice"):
+        rtx_mod.render_multi([d, d], cam, 1, 5)
+    with pytest.raises(rtx_mod.RtxError, match="stripe_count"):
+        rtx_mod.render_multi([d], cam, 1, 5, stripe_index=2, stripe_count=2)
+
+
+def test_encode_p3_matches_device_render_p3(rtx_mod, scenes):
+    _, d = scenes("cornell")
+    cam = rtx_mod.camera(rtx_mod.camera_config("cornell", width=30))
+    p3, _ = d.render_p3(cam, 4, 10, seed=2, adaptive=False, mode="persistent")
+    rgb, _, _ = d.render(cam, 4, 10, seed=2, adaptive=False, mode="persistent")
+    assert rtx_mod.encode_p3(d, rgb, cam.image_width, cam.image_height) == p3
+
+
+def test_schedule_timing_is_ordered_after_user_stream_work(rtx_mod, scenes):
+    """The first fast persistent render of a scene times its two schedules on scratch
+    buffers shared with every render: on the caller's stream, so a render still queued there
+    is not overwritten."""
+    import torch
+
+    path, _ = scenes("bunny")
+    cam = rtx_mod.camera(rtx_mod.camera_config("c3_bunny", width=160))
+    ref_dev = rtx_mod.DeviceScene(rtx_mod.HostScene.load(path))
+    want_a, _, _ = ref_dev.render(cam, 6, 20, seed=21, adaptive=False, mode="wavefront", precision="parity")
+    want_b, _, _ = ref_dev.render(cam, 6, 20, seed=22, adaptive=False, mode="persistent", precision="fast")
+    fresh = rtx_mod.DeviceScene(rtx_mod.HostScene.load(path))  # schedule not yet timed
+    npix = cam.image_width * cam.image_height
+    a = torch.empty((npix, 3), dtype=torch.float64, device="cuda:0")
+    b = torch.empty((npix, 3), dtype=torch.float64, device="cuda:0")
+    s = torch.cuda.Stream()
+    pa, pb = rtx_mod.RenderParams(), rtx_mod.RenderParams()
+    for p, seed, mode, prec in ((pa, 21, 0, 0), (pb, 22, 1, 1)):
+        p.spp, p.max_depth, p.adaptive, p.seed, p.mode, p.precision = 6, 20, 0, seed, mode, prec
+    # no stats: the first call returns with its render still queued on s
+    fresh.render_device(cam, pa, a.data_ptr(), 0, stream=s.cuda_stream, stats=False)
+    fresh.render_device(cam, pb, b.data_ptr(), 0, stream=s.cuda_stream, stats=False)  # times the schedules first
+    s.synchronize()
+    assert np.array_equal(a.cpu().numpy(), want_a)
+    assert np.array_equal(b.cpu().numpy(), want_b)
