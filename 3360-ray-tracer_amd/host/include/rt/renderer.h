@@ -25,7 +25,17 @@ class WavefrontRenderer {
   void Render();
   void Render(std::ostream& out);
 
+  ~WavefrontRenderer();
+  WavefrontRenderer(const WavefrontRenderer&) = delete;
+  WavefrontRenderer& operator=(const WavefrontRenderer&) = delete;
+
   // MI355X extensions (defaults reproduce the reference's semantics)
+  // Render one frame over `devices` (the integrator's device first): interleaved row
+  // stripes of `stripe_rows` rows, one host thread + stream per device, gathered into one
+  // host framebuffer and one P3 output (rtx_render_multi).  The pixels are the
+  // same for every device count.
+  void set_devices(const std::vector<int>& devices, int stripe_rows = 8);
+  void set_gpus(int n);  // devices 0 .. n-1 (the integrator's device first)
   void set_seed(uint64_t s) { params_.seed = s; }
   void set_adaptive(bool on) { params_.adaptive = on ? 1 : 0; }
   void set_mode(int mode) { params_.mode = mode; }
@@ -43,6 +53,9 @@ class WavefrontRenderer {
   std::vector<double> rgb_;
   std::vector<int32_t> spp_;
   rtx_stats stats_{};
+  std::vector<int> devices_;          // extra devices (besides the integrator's)
+  std::vector<rtx_scene*> extra_;     // their device-resident copies of the scene
+  int stripe_rows_ = 8;
 };
 
 // MegaKernel + DefaultSampler semantics (recursive GetPixel with the Scatter API, camera.h:

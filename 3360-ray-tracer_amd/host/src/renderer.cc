@@ -72,6 +72,30 @@ WavefrontRenderer::WavefrontRenderer(const scene::Scene& w, const scene::Camera&
                                      int max_depth, int max_samples, int /*batch_size*/)
     : world(w), cam(c), integrator(i), params_(DefaultParams(max_samples, max_depth)) {}
 
+WavefrontRenderer::~WavefrontRenderer() {
+  for (rtx_scene* s : extra_) rtx_scene_destroy(s);
+}
+
+void WavefrontRenderer::set_devices(const std::vector<int>& devices, int stripe_rows) {
+  for (rtx_scene* s : extra_) rtx_scene_destroy(s);
+  extra_.clear();
+  devices_ = devices;
+  stripe_rows_ = stripe_rows > 0 ? stripe_rows : 8;
+}
+
+void WavefrontRenderer::set_gpus(int n) {
+  int count = 0;
+  if (rtx_device_count(&count) != RTX_OK) throw std::runtime_error(std::string("rtx_device_count: ") + rtx_last_error());
+  if (n < 1 || n > count) throw std::invalid_argument("WavefrontRenderer::set_gpus: " + std::to_string(n) +
+                                                      " GPUs requested, " + std::to_string(count) + " present");
+  auto* gpu = dynamic_cast<integrator::GpuRayIntegrator*>(&integrator);
+  const int first = gpu ? gpu->device() : 0;
+  std::vector<int> d{first};
+  for (int k = 0; (int)d.size() < n; k++)
+    if (k != first) d.push_back(k);
+  set_devices(d, stripe_rows_);
+}
+
 void WavefrontRenderer::Render() { Render(std::cout); }
 
 void WavefrontRenderer::Render(std::ostream& out) {
@@ -90,6 +114,27 @@ void WavefrontRenderer::Render(std::ostream& out) {
   // wavefront.cc:238-241: the P3 text is formatted on the device (rtx_render_p3)
   std::string bytes(rtx_p3_max_bytes(dc.image_width, dc.image_height), '\0');
   size_t len = 0;
+  if (devices_.size() > 1) {  // one frame over several devices, gathered on the host
+    if (extra_.empty()) {
+      const rtx_scene_desc d = gpu->flat().desc();
+      for (size_t k = 1; k < devices_.size(); k++) {
+        rtx_scene* s = nullptr;
+        if (rtx_scene_create(devices_[k], &d, &s) != RTX_OK)
+          throw std::runtime_error(std::string("rtx_scene_create: ") + rtx_last_error());
+        extra_.push_back(s);
+      }
+    }
+    std::vector<rtx_scene*> all{gpu->device_scene()};
+    all.insert(all.end(), extra_.begin(), extra_.end());
+    p.stripe_rows = stripe_rows_, p.stripe_index = 0, p.stripe_count = 0;
+    if (rtx_render_multi(all.data(), (int32_t)all.size(), &dc, &p, rgb_.data(), spp_.data(), &stats_, nullptr) !=
+            RTX_OK ||
+        rtx_encode_p3(all[0], rgb_.data(), dc.image_width, dc.image_height, bytes.data(), bytes.size(), &len) !=
+            RTX_OK)
+      throw std::runtime_error(std::string("rtx_render_multi: ") + rtx_last_error());
+    out.write(bytes.data(), (std::streamsize)len);
+    return;
+  }
   if (rtx_render_p3(gpu->device_scene(), &dc, &p, bytes.data(), bytes.size(), &len, rgb_.data(), spp_.data(), &stats_) != RTX_OK)
     throw std::runtime_error(std::string("rtx_render_p3: ") + rtx_last_error());
   out.write(bytes.data(), (std::streamsize)len);

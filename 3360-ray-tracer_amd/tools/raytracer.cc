@@ -2,7 +2,10 @@
 //   raytracer [camera-preset] [--scene cornell|three|final|bunny|mixed|<file.rtxs>]
 //             [--cameras cameras.json] [--spp N] [--depth N] [--seed S] [--fixed]
 //             [--mode wavefront|persistent|megakernel] [--precision parity|fast]
-//             [--mk-adaptive MIN:THRESHOLD] > out.ppm
+//             [--mk-adaptive MIN:THRESHOLD] [--gpus N] > out.ppm
+// --gpus N renders one frame over N GPUs (interleaved row stripes, one host thread per GPU,
+// one gathered framebuffer and P3 output; identical pixels for every N); --devices 0,2,3
+// names the devices (a device may repeat: several streams on one GPU).
 // --mk-adaptive selects the AdaptiveSampler (sampler.h:44-82) for --mode megakernel,
 // with max_samples = the preset's (or --spp) samples.
 // Defaults follow main.cc: preset "default" (fallback when unknown), the Cornell box
@@ -14,6 +17,7 @@
 #include <iomanip>
 #include <iostream>
 #include <string>
+#include <vector>
 
 #include "rt/renderer.h"
 
@@ -26,7 +30,8 @@ int main(int argc, char** argv) {
   int spp = -1, depth = -1;
   uint64_t seed = 1234;
   bool fixed = false;
-  int mk_min = -1;
+  std::vector<int> devices;
+  int mk_min = -1, gpus = 1;
   float mk_thr = 0.0f;
   for (int i = 1; i < argc; i++) {
     std::string a = argv[i];
@@ -45,6 +50,16 @@ int main(int argc, char** argv) {
     else if (a == "--mode") mode = next();
     else if (a == "--precision") precision = next();
     else if (a == "--fixed") fixed = true;
+    else if (a == "--gpus") gpus = std::atoi(next().c_str());
+    else if (a == "--devices") {
+      const std::string v = next();
+      for (size_t p = 0; p < v.size();) {
+        size_t q = v.find(',', p);
+        if (q == std::string::npos) q = v.size();
+        devices.push_back(std::atoi(v.substr(p, q - p).c_str()));
+        p = q + 1;
+      }
+    }
     else if (a == "--mk-adaptive") {
       const std::string v = next();
       const size_t c = v.find(':');
@@ -90,12 +105,15 @@ int main(int argc, char** argv) {
       r.set_seed(seed);
       r.Render();
     } else {
-      integrator::GpuRayIntegrator integ(world.get(), 0, precision == "fast" ? RTX_PREC_FAST : RTX_PREC_PARITY);
+      integrator::GpuRayIntegrator integ(world.get(), devices.empty() ? 0 : devices[0],
+                                         precision == "fast" ? RTX_PREC_FAST : RTX_PREC_PARITY);
       renderer::WavefrontRenderer r(*world, cam, integ, md, ns, 2 * 8192);
       r.set_seed(seed);
       r.set_adaptive(!fixed);
       r.set_precision(precision == "fast" ? RTX_PREC_FAST : RTX_PREC_PARITY);
       r.set_mode(mode == "persistent" ? RTX_MODE_PERSISTENT : RTX_MODE_WAVEFRONT);
+      if (!devices.empty()) r.set_devices(devices);
+      else if (gpus > 1) r.set_gpus(gpus);
       r.Render();
       std::clog << "Rays: " << r.stats().rays_total << " (" << r.stats().rays_total / (r.stats().kernel_ms * 1e3)
                 << " Mrays/s device)\n";
