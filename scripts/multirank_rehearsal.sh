@@ -1,5 +1,6 @@
 #!/bin/bash
-# bench.py's N>1 path on a single GPU: 2 ranks (gloo barrier/reductions) sharing cuda:0.
+# bench.py's N>1 path on a single GPU: 2 ranks (gloo barrier/reductions) sharing cuda:0,
+# rendering one C4 frame split in stripes into the shared /dev/shm framebuffer.
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 mkdir -p gpurun_out
 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
