@@ -98,6 +98,7 @@ struct rtx_scene {
   std::vector<DevBuf> texels;
   DScene S{};
   int stack_parity = 32, stack_fast = 32;
+  int fast_need = 0;     // exact worst-case stack depth of the lean BVH4 walk (build_fast4)
   bool fast_ok = false;  // RTX_PREC_FAST available (BVH with an internal root)
   int park = -1;         // persistent fast schedule: -1 not yet timed, 0 plain kernel, 1 PARK kernel
   DevBuf calib_rgb;      // output of the schedule-timing renders
@@ -556,7 +557,8 @@ int run_extend(const Launch& L, const RenderArgs& A, const PathQueue& q, const u
 template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK, bool LAMB = false, bool NOTEX = false,
           bool NODOF = false>
 int run_persistent_k0(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
-  const size_t lds = stack_lds_bytes(STACK);
+  if (A.stack_slots < 1 || A.stack_slots > STACK + 1) return fail(RTX_ERR_INVALID, "bad traversal stack size");
+  const size_t lds = persistent_lds_bytes(A.stack_slots);
   const int grid = persistent_grid(
       L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF>, lds);
   L.build = (PARK ? RTX_BUILD_PARK : 0u) | (TK == (int)RTX_PRIM_SPHERE ? RTX_BUILD_SPHERE_TREE : 0u) |
@@ -772,6 +774,7 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
       const int need = build_fast4(d->nodes, d->prims, f4);
 #endif
       sc->stack_fast = need < 0 ? -1 : (need <= 32 ? 32 : (need <= 64 ? 64 : -1));
+      sc->fast_need = need;
       if (sc->stack_fast > 0 && (rc = upload(sc->fnodes, f4.data(), f4.size(), s))) return rc;
 #else
       build_fast(d->nodes, d->n_nodes, fn);
@@ -990,6 +993,9 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
   A.conv = prm->adaptive ? sc->px_conv.as<uint8_t>() : nullptr;
   A.L = sc->lbuf.as<double>();
   A.counters = cnt;
+  // the lean BVH4 walk stores at most fast_need + 1 stack slots (RTX_PUSH_BRANCHLESS); the
+  // parity walk gets its template bound (pick_stack: reference depth + 2)
+  A.stack_slots = (fast && RTX_NODE_LEAN && RTX_PUSH_BRANCHLESS) ? sc->fast_need + 1 : L.stack + 1;
   // counters[8..] : queue counts (u32) for the wavefront, [16] slot counter (persistent)
   unsigned* qcount = (unsigned*)(cnt + 8);
   unsigned long long* next_slot = cnt + 16;

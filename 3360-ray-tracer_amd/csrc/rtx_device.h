@@ -1368,27 +1368,46 @@ __device__ __forceinline__ V3 normalize_l(V3 v, double& l) {
 // in the same IEEE double operations (device material table, rtx_scene_create).
 // LAMB: every material of the scene is Lambertian (DScene::all_lambertian; the bunny), so the
 // metal / dielectric / emitter branches are compiled out.  Same operations for a Lambertian.
-template <bool LAMB = false, bool NOTEX = false>
-__device__ __forceinline__ bool shade_merged(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit,
-                                             Rng& g, V3& L, const rtx_material& m) {
-  L = v3(0, 0, 0);
+// What one shading step decided, before the path throughput is applied (shade_finish):
+// the core of the step never reads the throughput, so a caller may keep it out of registers
+// (the persistent kernel parks it in LDS while the lane walks the tree).
+enum : int32_t {
+  kShadeEmit = 0,     // terminated, L = thr * f (sky on a miss / at the depth limit, or emission)
+  kShadeDead = 1,     // terminated, L = 0 (absorbed: Sample() failed, pdf < 1e-6f, DiffuseLight)
+  kShadeDiffuse = 2,  // continues, thr' = ((double)ct * (thr * f)) / (double)pdf (wavefront.cc:180-185)
+  kShadeSpecular = 3  // continues, thr' = thr * f (IsSpecular)
+};
+struct ShadeOut {
+  V3 f;
+  float ct, pdf;
+  int32_t what;
+};
+
+// SET_ORIGIN = false: a continuing path's new origin (the hit point) is left for the caller
+// to set, so a caller that parked the hit point elsewhere keeps rec.p out of registers.
+template <bool LAMB = false, bool NOTEX = false, bool SET_ORIGIN = true>
+__device__ __forceinline__ void shade_core(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit, Rng& g,
+                                           const rtx_material& m, ShadeOut& so) {
+  so.what = kShadeDead;
   double lnd;
   const V3 nd = normalize_l(p.d, lnd);  // wo = -nd (hit), sky(d) (miss)
   if (!hit || p.depth >= max_depth) {
     const double t = 0.5 * (nd.y + 1.0);  // sky() with ud = nd
-    L = L + p.thr * ((1.0 - t) * v3(1.0, 1.0, 1.0) + t * v3(0.5, 0.7, 1.0));
-    return false;
+    so.f = (1.0 - t) * v3(1.0, 1.0, 1.0) + t * v3(0.5, 0.7, 1.0);
+    so.what = kShadeEmit;
+    return;
   }
   if (!LAMB) {  // Lambertian emits nothing (Material::Emitted default, material.h:50-54)
     V3 em = mat_emitted_t<NOTEX>(S, m, rec);
     if (!near_zero(em)) {
-      L = L + p.thr * em;
-      return false;
+      so.f = em;
+      so.what = kShadeEmit;
+      return;
     }
   }
   const int kind = LAMB ? (int)RTX_MAT_LAMBERTIAN : m.kind;
   const bool isL = kind == RTX_MAT_LAMBERTIAN, isM = kind == RTX_MAT_METAL, isG = kind == RTX_MAT_DIELECTRIC;
-  if (!(isL || isM || isG)) return false;  // DiffuseLight::Sample
+  if (!(isL || isM || isG)) return;  // DiffuseLight::Sample
   const V3 n = rec.normal;
   double r1 = 0.0, r2 = 0.0;
   if (isL) r1 = g.next(), r2 = g.next();
@@ -1449,45 +1468,67 @@ __device__ __forceinline__ bool shade_merged(const DScene& S, int max_depth, Pat
   double l4;
   V3 s4 = normalize_l(in4, l4);
   pin(s4);
-  V3 wi, f;
-  Path c;
-  c.o = rec.p, c.depth = p.depth + 1;
+  V3 wi;
   if (isL) {
     const V3 v = s4;
     const V3 u = cross(v, w);
     // ---- slot 5: normalize (Lambertian only)
     wi = normalize(x * u + y * v + s3 * w);
-    if (dot(wi, n) <= 0) return false;
+    if (dot(wi, n) <= 0) return;
     const float cf = (float)dot(n, wi);
     const float pdf = (cf <= 0.0f) ? 0.0f : (float)((double)cf / kPi);
-    f = mat_tex_t<NOTEX>(S, m, rec) / kPi;
-    if (pdf < 1e-6f) return false;
-    const float ct = fmaxf(0.0f, (float)dot(wi, n));
-    c.thr = ((double)ct * (p.thr * f)) / (double)pdf;
+    so.f = mat_tex_t<NOTEX>(S, m, rec) / kPi;
+    if (pdf < 1e-6f) return;
+    so.ct = fmaxf(0.0f, (float)dot(wi, n));
+    so.pdf = pdf;
+    so.what = kShadeDiffuse;
   } else if (isM) {
     wi = s4;
-    if (dot(wi, n) <= 0) return false;
-    c.thr = p.thr * v3(m.albedo[0], m.albedo[1], m.albedo[2]);
+    if (dot(wi, n) <= 0) return;
+    so.f = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
+    so.what = kShadeSpecular;
   } else {
     if (g_reflect) {
       wi = reflect(win, n);
-      c.thr = p.thr * v3(1.0, 1.0, 1.0);
+      so.f = v3(1.0, 1.0, 1.0);
     } else {
       const V3 par = (-s3) * n;
       wi = perp + par;
       const double k = eta * eta;
-      c.thr = p.thr * v3(k, k, k);
+      so.f = v3(k, k, k);
     }
+    so.what = kShadeSpecular;
   }
-  c.d = wi;
-  if (c.depth > 5) {  // Russian roulette (wavefront.cc:189-205)
-    double q = fmax(fmax(c.thr.x, c.thr.y), c.thr.z);
+  if (SET_ORIGIN) p.o = rec.p;
+  p.d = wi, p.depth = p.depth + 1;
+}
+
+// The rest of the step: radiance of a terminated path, or the child's throughput and Russian
+// roulette (wavefront.cc:189-205) with the segment's last draw.  depth = the child's depth.
+__device__ __forceinline__ bool shade_finish(const ShadeOut& so, V3& thr, int32_t depth, Rng& g, V3& L) {
+  L = v3(0, 0, 0);
+  if (so.what == kShadeEmit) {
+    L = L + thr * so.f;
+    return false;
+  }
+  if (so.what == kShadeDead) return false;
+  V3 c = so.what == kShadeDiffuse ? ((double)so.ct * (thr * so.f)) / (double)so.pdf : thr * so.f;
+  if (depth > 5) {
+    double q = fmax(fmax(c.x, c.y), c.z);
     q = q < 0.1 ? 0.1 : (q > 0.95 ? 0.95 : q);
     if (g.next() > q) return false;
-    c.thr = c.thr / q;
+    c = c / q;
   }
-  p = c;
+  thr = c;
   return true;
+}
+
+template <bool LAMB = false, bool NOTEX = false>
+__device__ __forceinline__ bool shade_merged(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit,
+                                             Rng& g, V3& L, const rtx_material& m) {
+  ShadeOut so;
+  shade_core<LAMB, NOTEX>(S, max_depth, p, rec, hit, g, m, so);
+  return shade_finish(so, p.thr, p.depth, g, L);
 }
 
 // The same step with one Sample() branch per material (mat_sample): the reference's

@@ -87,6 +87,7 @@ struct RenderArgs {
   const uint8_t* conv;  // per-pixel converged flag (adaptive), may be null
   double* L;            // Lbuf: 3 doubles per slot
   unsigned long long* counters;  // [0] segments [1] primaries [2] node visits [3] prim tests
+  int32_t stack_slots;  // persistent kernel: traversal-stack slots per lane in LDS (the walk's exact bound + 1)
 };
 
 // Per-sample radiance of group slot (pixel p, group sample k) = slot p*K+k, channel c.
@@ -121,6 +122,22 @@ __device__ __forceinline__ int64_t wave_compact(bool want, unsigned int* counter
 // LDS of a block's traversal stacks: STACK + 1 slots per lane (the branchless pushes of the
 // lean walk may store one slot above the deepest entry, see trace4_run).
 constexpr size_t stack_lds_bytes(int STACK) { return (size_t)(STACK + 1) * kBlock * sizeof(uint32_t); }
+#ifndef RTX_THR_LDS
+#define RTX_THR_LDS 1  // persistent: path throughput parked in LDS across the traversal (no VGPR spill of it)
+#endif
+#ifndef RTX_HITP_LDS
+#define RTX_HITP_LDS 1  // persistent, texture-free builds: the hit point parked in LDS across the BSDF sampling
+#endif
+// The persistent kernel's LDS per block: the traversal stacks (stack_slots per lane, the
+// walk's exact bound + 1), then each lane's path throughput (RTX_THR_LDS) and hit point
+// (RTX_HITP_LDS), 3 doubles each, channel-major (lane-consecutive 8-byte words: conflict-
+// free).  Shading reads the throughput only at its end and the hit point only as the next
+// origin, so both stay in LDS while the lane walks the tree and samples the BSDF instead of
+// occupying 12 of the 128 VGPRs a lane has at 4 waves per SIMD (or spilling to scratch).
+constexpr int kLdsThr = RTX_THR_LDS ? 3 : 0, kLdsHitP = RTX_HITP_LDS ? 3 : 0;
+constexpr size_t persistent_lds_bytes(int stack_slots) {
+  return (size_t)stack_slots * kBlock * sizeof(uint32_t) + (size_t)(kLdsThr + kLdsHitP) * kBlock * sizeof(double);
+}
 
 template <int STACK, bool FAST, bool COUNT, int TK = -1>
 __device__ __forceinline__ int64_t trace(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
@@ -316,6 +333,10 @@ template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK = -1
 __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderArgs A, unsigned long long* next_slot) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* stk = lds + threadIdx.x;
+  double* thr_lds = (double*)(lds + A.stack_slots * kBlock) + threadIdx.x;  // [c * kBlock] (RTX_THR_LDS)
+  double* hitp_lds = thr_lds + kLdsThr * kBlock;                             // [c * kBlock] (RTX_HITP_LDS)
+  constexpr bool kHitpLds = RTX_HITP_LDS && NOTEX && !SCATTER && RTX_MERGED_SHADE;  // nothing else reads rec.p
+  (void)hitp_lds;
   const uint64_t nslots = (uint64_t)A.npix * (uint64_t)A.K;
   // GetPixel uses Interval(0.001, inf) (camera.h:158); IntersectBatch uses 0.001f (cpu_ray_integrator.h:21)
   const double tmin = SCATTER ? 0.001 : (double)0.001f;
@@ -390,7 +411,11 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
         pix = (uint32_t)(y * A.map.W + x), smp = (uint32_t)(A.s0 + k);
         Rng g = make_rng(A.seed, pix, smp, 0u);
         get_ray<NODOF>(A.cam, x, y, g, P.o, P.d);
+#if RTX_THR_LDS
+        thr_lds[0] = 1.0, thr_lds[kBlock] = 1.0, thr_lds[2 * kBlock] = 1.0;
+#else
         P.thr = v3(1.0, 1.0, 1.0);
+#endif
         P.depth = SCATTER ? A.max_depth : 0;
         has = true;
         prims++;
@@ -438,8 +463,12 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
       if (best >= 0) m = A.S.mats[bmat];
 #endif
       if (best >= 0) finish_hit_at<false>(A.S, best, tb, P.o, P.d, h);
+      if (kHitpLds && best >= 0) hitp_lds[0] = h.p.x, hitp_lds[kBlock] = h.p.y, hitp_lds[2 * kBlock] = h.p.z;
 #if !RTX_EARLY_MAT
       if (best >= 0) m = A.S.mats[h.mat];
+#endif
+#if RTX_THR_LDS
+      if (SCATTER) P.thr = v3(thr_lds[0], thr_lds[kBlock], thr_lds[2 * kBlock]);
 #endif
       // stream of this segment: depth + 1 (GetPixel: depth counts down from max_depth)
       Rng g = make_rng(A.seed, pix, smp, SCATTER ? (uint32_t)(A.max_depth - P.depth) + 1u : (uint32_t)P.depth + 1u);
@@ -463,8 +492,25 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
           }
         }
       } else {
+#if RTX_THR_LDS && RTX_MERGED_SHADE
+        // the throughput is read from LDS only after the shading core: none of its registers
+        // are live across the walk or the BSDF sampling
+        ShadeOut so;
+        shade_core<LAMB, NOTEX, !kHitpLds>(A.S, A.max_depth, P, h, best >= 0, g, m, so);
+        V3 thr = v3(thr_lds[0], thr_lds[kBlock], thr_lds[2 * kBlock]);
+        cont = shade_finish(so, thr, P.depth, g, L);
+        if (cont) thr_lds[0] = thr.x, thr_lds[kBlock] = thr.y, thr_lds[2 * kBlock] = thr.z;
+        if (kHitpLds && cont) P.o = v3(hitp_lds[0], hitp_lds[kBlock], hitp_lds[2 * kBlock]);
+#else
+#if RTX_THR_LDS
+        P.thr = v3(thr_lds[0], thr_lds[kBlock], thr_lds[2 * kBlock]);
+#endif
         cont = shade<LAMB, NOTEX>(A.S, A.max_depth, P, h, best >= 0, g, L, m);
+#endif
       }
+#if RTX_THR_LDS
+      if (SCATTER && cont) thr_lds[0] = P.thr.x, thr_lds[kBlock] = P.thr.y, thr_lds[2 * kBlock] = P.thr.z;
+#endif
     }
     RTX_STAMP(2)
     if (!cont) {
