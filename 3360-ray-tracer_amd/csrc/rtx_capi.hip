@@ -813,6 +813,7 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
     S.tree_kind = k < 0 ? -1 : k;
   }
   S.global[0] = global[0], S.global[1] = global[1];
+  S.pool_ok = d->n_prims < (1ll << 26) ? 1 : 0;
   for (int64_t i = 0; i < d->n_prims && !S.has_tris; i++) S.has_tris = d->prims[i].kind == RTX_PRIM_TRIANGLE;
   if (S.use_bvh && d->nodes[0].is_leaf) S.froot_leaf = 1, S.froot_count = (int32_t)d->nodes[0].right_count;
   if (!d->nodes && d->n_nodes == 0) S.use_bvh = 0;
@@ -1119,6 +1120,13 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
       fprintf(stderr, "rtx tail: node-loop wave iterations %llu; fraction with <=1/2/4/8/16/32 active lanes:", h[4]);
       for (int i = 0; i < 6; i++) fprintf(stderr, " %.4f", (double)th[i] / (double)h[4]);
       fprintf(stderr, "\n");
+      unsigned long long lh[5];
+      HIPC(hipMemcpy(lh, cnt + 46, sizeof lh, hipMemcpyDeviceToHost));
+      const double ph = (double)(lh[0] + lh[1] + lh[2] + lh[3]);
+      fprintf(stderr, "rtx leaf: node iterations with leaf tests %.0f (%.4f of node-loop iterations); leaf-loop length "
+              "1/2/3/4: %.4f %.4f %.4f %.4f; leaf tests per such iteration %.2f; leaf-loop wave iterations %.0f\n",
+              ph, ph / (double)h[4], lh[0] / ph, lh[1] / ph, lh[2] / ph, lh[3] / ph, (double)lh[4] / ph,
+              (double)(lh[0] + 2 * lh[1] + 3 * lh[2] + 4 * lh[3]));
     }
 #endif
 #if RTX_STAMPS

@@ -135,16 +135,19 @@ constexpr size_t stack_lds_bytes(int STACK) { return (size_t)(STACK + 1) * kBloc
 // origin, so both stay in LDS while the lane walks the tree and samples the BSDF instead of
 // occupying 12 of the 128 VGPRs a lane has at 4 waves per SIMD (or spilling to scratch).
 constexpr int kLdsThr = RTX_THR_LDS ? 3 : 0, kLdsHitP = RTX_HITP_LDS ? 3 : 0;
+// ... and the pooled leaf tests' candidate lists (RTX_LEAF_POOL): kPoolWords per wave
+constexpr size_t kLdsPool = RTX_LEAF_POOL ? (size_t)(kBlock / 64) * kPoolWords * sizeof(uint32_t) : 0;
 constexpr size_t persistent_lds_bytes(int stack_slots) {
-  return (size_t)stack_slots * kBlock * sizeof(uint32_t) + (size_t)(kLdsThr + kLdsHitP) * kBlock * sizeof(double);
+  return (size_t)stack_slots * kBlock * sizeof(uint32_t) + (size_t)(kLdsThr + kLdsHitP) * kBlock * sizeof(double) +
+         kLdsPool;
 }
 
 template <int STACK, bool FAST, bool COUNT, int TK = -1>
 __device__ __forceinline__ int64_t trace(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
-                                         Counters& c, double& t_best, int32_t& mat_best) {
+                                         Counters& c, double& t_best, int32_t& mat_best, uint32_t* pool = nullptr) {
 #if RTX_BVH4
 #if RTX_NODE_LEAN
-  if (FAST) return trace_fast4_lean<STACK, COUNT, TK>(S, o, d, tmin, tmax, stk, kBlock, c, t_best, mat_best);
+  if (FAST) return trace_fast4_lean<STACK, COUNT, TK>(S, o, d, tmin, tmax, stk, kBlock, c, t_best, mat_best, pool);
 #else
   if (FAST) return trace_fast4<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best, mat_best);
 #endif
@@ -174,6 +177,8 @@ __device__ __forceinline__ void flush_counters(const RenderArgs& A, const Counte
     atomicAdd(&A.counters[7], (unsigned long long)c.sphs);
 #if RTX_TAILHIST
     for (int i = 0; i < 6; i++) atomicAdd(&A.counters[40 + i], (unsigned long long)c.tail[i]);
+    for (int i = 0; i < 4; i++) atomicAdd(&A.counters[46 + i], (unsigned long long)c.leafph[i]);
+    atomicAdd(&A.counters[50], (unsigned long long)c.leaft);
 #endif
   }
   if (segs) atomicAdd(&A.counters[0], (unsigned long long)segs);
@@ -193,7 +198,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_intersect(DScene S,
   if (i >= n) return;
   const rtx_ray r = rays[i];
   V3 o{r.origin[0], r.origin[1], r.origin[2]}, d{r.direction[0], r.direction[1], r.direction[2]};
-  Counters c{0, 0, 0, 0, 0, 0};
+  Counters c{};
   double tb;
   const int64_t best = trace<STACK, FAST, false>(S, o, d, tmin, tmax, stk, c, tb);
   rtx_hit out;
@@ -245,7 +250,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_generate(RenderArgs A, PathQueue 
       q.meta[dst] = 0u;  // depth 0
     }
   }
-  flush_counters(A, Counters{0, 0, 0, 0, 0, 0}, 0, made, false);
+  flush_counters(A, Counters{}, 0, made, false);
 }
 #endif
 
@@ -256,7 +261,7 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_wf_extend(RenderArg
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* stk = lds + threadIdx.x;
   const int64_t n = *count;
-  Counters c{0, 0, 0, 0, 0, 0};
+  Counters c{};
   uint32_t segs = 0;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t)gridDim.x * kBlock) {
     const V3 o = v3(q.ox[i], q.oy[i], q.oz[i]);
@@ -337,10 +342,15 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
   double* hitp_lds = thr_lds + kLdsThr * kBlock;                             // [c * kBlock] (RTX_HITP_LDS)
   constexpr bool kHitpLds = RTX_HITP_LDS && NOTEX && !SCATTER && RTX_MERGED_SHADE;  // nothing else reads rec.p
   (void)hitp_lds;
+  // this wave's pooled-leaf-test list (after the throughput and hit-point areas)
+  uint32_t* pool = (FAST && RTX_LEAF_POOL && A.S.pool_ok)
+                       ? (uint32_t*)(lds + A.stack_slots * kBlock + 2 * (kLdsThr + kLdsHitP) * kBlock) +
+                             (threadIdx.x >> 6) * kPoolWords
+                       : nullptr;
   const uint64_t nslots = (uint64_t)A.npix * (uint64_t)A.K;
   // GetPixel uses Interval(0.001, inf) (camera.h:158); IntersectBatch uses 0.001f (cpu_ray_integrator.h:21)
   const double tmin = SCATTER ? 0.001 : (double)0.001f;
-  Counters c{0, 0, 0, 0, 0, 0};
+  Counters c{};
   uint32_t segs = 0, prims = 0;
   uint64_t chunk_base = 0, chunk_left = 0;  // wave-uniform
   bool exhausted = false;                   // wave-uniform
@@ -445,14 +455,14 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
         }
         // parking only when some lane of this round finishes first: every round makes progress
         const bool done = trace4_run<STACK, COUNT, TK>(A.S, P.o, P.d, tmin, stk, kBlock, c, trs,
-                                                   active > RTX_PARK ? RTX_PARK : -1);
+                                                   active > RTX_PARK ? RTX_PARK : -1, pool);
         parked = !done;
         if (parked) continue;
         best = trs.best, tb = trs.closest, bmat = trs.mat;
       } else if (kPark) {  // no BVH, or its root is a leaf
         best = trace_flat(A.S, P.o, P.d, tmin, kInf, c, COUNT, tb, bmat);
       } else {
-        best = trace<STACK, FAST, COUNT, TK>(A.S, P.o, P.d, tmin, kInf, stk, c, tb, bmat);
+        best = trace<STACK, FAST, COUNT, TK>(A.S, P.o, P.d, tmin, kInf, stk, c, tb, bmat, pool);
       }
       RTX_STAMP(1)
       segs++;
