@@ -14,10 +14,9 @@
 
 namespace rt::scene {
 
-// Image (scene/image.h): texels after the reference's decode (stb, gamma 2.2) and
-// FloatToByte (image.cc:43-73).  The MI355X build ships those bytes as a binary PPM (P6)
-// produced once from the reference's own decoder (oracle/gen_golden.py), because no JPEG
-// decoder is part of this build.  Missing file -> Height() == 0 (cyan, texture.h:62).
+// Image (scene/image.h): texels after the reference's decode (stb_image's stbi_loadf: 8-bit
+// decode, gamma 2.2) and FloatToByte (image.cc:16-73), decoded by rt/image.h (JPEG, binary
+// PNM).  A file that does not load -> Height() == 0 (cyan, texture.h:62).
 class Image {
  public:
   Image() = default;
@@ -78,7 +77,7 @@ class CheckerTexture : public Texture {
 
 class ImageTexture : public Texture {
  public:
-  // "earthmap.jpg" resolves to the shipped texel dump "earthmap.ppm" (see scene::Image).
+  // the file name is resolved like image.cc:16-41 (as given, then the asset directories)
   explicit ImageTexture(const char* filename);
   TextureKind Kind() const override { return TextureKind::kImage; }
   const scene::Image& image() const { return *image_; }

@@ -5,6 +5,7 @@
 #include <stdexcept>
 #include <string>
 
+#include "rt/image.h"
 #include "rt/scene.h"
 #include "rtx.h"
 
@@ -164,3 +165,20 @@ int rtx_camera_config_load(const char* json_path, const char* preset, rtx_camera
 }
 
 }  // extern "C"
+
+// Image::Load (scene/image.cc:16-73) as a C entry point: the texels the renderer samples, or
+// (linear8) the 8-bit decode before stb's gamma step.  texels == NULL: size query.
+int rtx_image_load(const char* path, int32_t linear8, int32_t* width, int32_t* height, uint8_t* texels,
+                   size_t cap) {
+  if (!path || !width || !height) return host_fail(RTX_ERR_INVALID, "NULL argument");
+  int w = 0, h = 0;
+  std::vector<uint8_t> px;
+  std::string err;
+  if (!rt::scene::LoadTexels(path, w, h, px, err, linear8 != 0)) return host_fail(RTX_ERR_IO, err);
+  *width = w, *height = h;
+  if (texels) {
+    if (cap < px.size()) return host_fail(RTX_ERR_INVALID, "texel buffer too small");
+    std::memcpy(texels, px.data(), px.size());
+  }
+  return RTX_OK;
+}

@@ -7,6 +7,7 @@
 #include <stdexcept>
 #include <unordered_map>
 
+#include "rt/image.h"
 #include "rt/scene.h"
 
 #ifndef RTX_ASSET_DIR_DEFAULT
@@ -47,23 +48,19 @@ Image::Image(const std::string& filename) {
   if (!Load(filename)) std::cerr << "ERROR: Could not load image '" << filename << "'\n";  // image.cc:11-13
 }
 
+// image.cc:16-41: the file as named, then the image directory (here $RTX_ASSET_DIR and the
+// package's assets/); decoded like stbi_loadf + FloatToByte (rt/image.h).
 bool Image::Load(const std::string& filename) {
-  // P6 texel dump (see rt/material.h); "<stem>.jpg" maps to "<stem>.ppm".
-  std::string name = filename;
-  const size_t dot = name.rfind('.');
-  if (dot != std::string::npos && name.substr(dot) != ".ppm") name = name.substr(0, dot) + ".ppm";
-  const std::string path = ResolveAsset(name);
+  const std::string path = ResolveAsset(filename);
   if (path.empty()) return false;
-  std::ifstream in(path, std::ios::binary);
-  std::string magic;
-  int w = 0, h = 0, maxv = 0;
-  in >> magic >> w >> h >> maxv;
-  in.get();
-  if (!in || magic != "P6" || maxv != 255 || w <= 0 || h <= 0) return false;
-  std::vector<unsigned char> b((size_t)w * h * 3);
-  in.read((char*)b.data(), (std::streamsize)b.size());
-  if (!in) return false;
-  width_ = w, height_ = h, bdata_ = std::move(b);
+  int w = 0, h = 0;
+  std::vector<unsigned char> texels;
+  std::string err;
+  if (!LoadTexels(path, w, h, texels, err)) {
+    std::cerr << "image " << path << ": " << err << "\n";
+    return false;
+  }
+  width_ = w, height_ = h, bdata_ = std::move(texels);
   return true;
 }
 

@@ -66,10 +66,12 @@ std::shared_ptr<Scene> LoadSceneFile(const std::string& path, const std::string&
       } else if (kind == "image") {
         std::string name;
         ss >> name;
-        // image names are resolved against asset_dir first (RTX_ASSET_DIR / package assets after)
-        std::string p = join(asset_dir, name + ".ppm");
+        // an image name without extension is the reference's "<name>.jpg" (main.cc:65); names
+        // are resolved against asset_dir first (RTX_ASSET_DIR / package assets after)
+        if (name.find('.') == std::string::npos) name += ".jpg";
+        std::string p = join(asset_dir, name);
         std::ifstream probe(p);
-        tex.push_back(std::make_shared<material::ImageTexture>((probe ? p : name + ".jpg").c_str()));
+        tex.push_back(std::make_shared<material::ImageTexture>((probe ? p : name).c_str()));
       } else {
         bad("unknown texture kind " + kind);
       }
@@ -285,7 +287,7 @@ std::shared_ptr<Scene> BuildRecipe(const std::string& name, uint32_t seed, const
     w.Add(std::make_shared<geom::Sphere>(Point3(0, -1003.9, 0), 1000, lambert(R, Color(0.5, 0.5, 0.5))));
   } else if (name == "mixed") {  // main.cc:72-145 Spheres(), SeedRng(seed)
     core::SeedRng(seed);
-    std::string tp = join(asset_dir, "earthmap.ppm");
+    std::string tp = join(asset_dir, "earthmap.jpg");
     std::ifstream probe(tp);
     auto earth_tex = reg<material::ImageTexture>(R, (probe ? tp : std::string("earthmap.jpg")).c_str());
     auto earth = reg<material::Lambertian>(R, std::static_pointer_cast<material::Texture>(earth_tex));

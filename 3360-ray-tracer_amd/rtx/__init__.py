@@ -113,7 +113,7 @@ EXPORTS = ["rtx_abi_version", "rtx_last_error", "rtx_device_count", "rtx_scene_c
            "rtx_render_device", "rtx_host_scene_load", "rtx_host_scene_recipe", "rtx_host_scene_write",
            "rtx_host_scene_desc", "rtx_host_scene_prim_indices", "rtx_host_scene_destroy",
            "rtx_camera_config_load", "rtx_write_ppm", "rtx_p3_max_bytes", "rtx_render_p3", "rtx_encode_p3_device",
-           "rtx_prim_bounds", "rtx_bvh_build", "rtx_bvh_build_host", "rtx_render_multi", "rtx_encode_p3"]
+           "rtx_prim_bounds", "rtx_bvh_build", "rtx_bvh_build_host", "rtx_render_multi", "rtx_encode_p3", "rtx_image_load"]
 
 _lib = None
 
@@ -157,6 +157,7 @@ def lib():
             "rtx_render_multi": ([C.POINTER(vp), i32, C.POINTER(Camera), C.POINTER(RenderParams), vp, vp,
                                   C.POINTER(Stats), vp], C.c_int),
             "rtx_encode_p3": ([vp, vp, i32, i32, vp, sz, C.POINTER(sz)], C.c_int),
+            "rtx_image_load": ([C.c_char_p, i32, C.POINTER(i32), C.POINTER(i32), vp, sz], C.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -374,6 +375,16 @@ def encode_p3(scene, rgb, width, height):
     _check(lib().rtx_encode_p3(scene.h, rgb.ctypes.data_as(C.c_void_p), width, height, buf, cap, C.byref(n)),
            "rtx_encode_p3")
     return buf.raw[:n.value]
+
+
+def image_load(path, linear8=False):
+    """Image::Load through rtx_image_load: (height, width, 3) uint8 texels (or the 8-bit decode)."""
+    w, h = C.c_int32(), C.c_int32()
+    _check(lib().rtx_image_load(path.encode(), int(linear8), C.byref(w), C.byref(h), None, 0), "rtx_image_load")
+    out = np.zeros((h.value, w.value, 3), np.uint8)
+    _check(lib().rtx_image_load(path.encode(), int(linear8), C.byref(w), C.byref(h),
+                                out.ctypes.data_as(C.c_void_p), out.nbytes), "rtx_image_load")
+    return out
 
 
 def prim_bounds(prims):

@@ -296,6 +296,14 @@ int rtx_host_scene_desc(const rtx_host_scene* s, rtx_scene_desc* out);
 int rtx_host_scene_prim_indices(const rtx_host_scene* s, int32_t* out, int64_t n);
 int rtx_host_scene_destroy(rtx_host_scene* s);
 
+/* Image::Load (scene/image.cc:16-73; stb_image's stbi_loadf + FloatToByte): decode an image
+   file — JPEG (sequential or progressive, 8-bit, 1/3/4 components) or binary PNM (P5/P6) — to
+   the RGB8 texels image textures sample (width * height * 3 bytes, rows top-down).
+   linear8 = 1: the 8-bit decode before the gamma-2.2 / FloatToByte step (stbi_load's bytes).
+   texels == NULL: only *width / *height.  RTX_ERR_IO for an unreadable or unsupported file. */
+int rtx_image_load(const char* path, int32_t linear8, int32_t* width, int32_t* height, uint8_t* texels,
+                   size_t cap);
+
 /* cameras.json preset -> config (parseCamera/loadCameras, scene/camera.h:40-67). */
 int rtx_camera_config_load(const char* json_path, const char* preset, rtx_camera_config* out);
 

@@ -14,7 +14,7 @@ and writes small fixtures (inputs + expected outputs) under tests/golden/:
   aabb.npz               Aabb::Hit cases incl. axis-parallel / NaN rays
   material.npz, scatter.npz, texture.npz, pixelstate.npz
   render_<case>.npz      seeded single-thread renders (mt RNG): linear fb, spp, P3 PPM bytes
-  earthmap texels        written to 3360-ray-tracer_amd/assets/earthmap.ppm (sha in golden)
+  textures/earthmap.ppm  the reference's decoded earthmap texels (Image after stb + FloatToByte)
 
 Nothing here is imported at run time by the product.  Re-run after changing the harness.
 """
@@ -124,8 +124,10 @@ def main():
 
     # assets: the bunny model is reference data; texels are the reference's stb decode
     shutil.copyfile(os.path.join(MODELS, "stanford-bunny.obj"), os.path.join(ASSETS, "stanford-bunny.obj"))
-    run("texels", os.path.join(ASSETS, "earthmap.ppm"))
-    meta = {"earthmap_ppm_sha256": sha(os.path.join(ASSETS, "earthmap.ppm")),
+    shutil.copyfile(os.path.join(REF, "textures", "earthmap.jpg"), os.path.join(ASSETS, "earthmap.jpg"))
+    os.makedirs(os.path.join(GOLD, "textures"), exist_ok=True)
+    run("texels", os.path.join(GOLD, "textures", "earthmap.ppm"))
+    meta = {"earthmap_ppm_sha256": sha(os.path.join(GOLD, "textures", "earthmap.ppm")),
             "bunny_obj_sha256": sha(os.path.join(ASSETS, "stanford-bunny.obj"))}
 
     out = subprocess.run([HARNESS, "rng", "1234", "64"], check=True, capture_output=True, text=True).stdout

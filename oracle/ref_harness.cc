@@ -38,6 +38,7 @@
 #include "material/material.h"
 #include "material/texture.h"
 #include "scene/image.h"
+#include "third-party/stb/stb_image.h"  // declarations only: stbi_load for the image8 command
 #include "scene/scene.h"
 
 #include <omp.h>
@@ -859,6 +860,27 @@ int main(int argc, char** argv) {
       out[3 * i] = v.x(), out[3 * i + 1] = v.y(), out[3 * i + 2] = v.z();
     }
     write_bin(argv[3], out);
+  } else if ((cmd == "image8" || cmd == "imagebytes") && argc == 4) {
+    // image8: the reference's 8-bit decode (stbi_load, 3 channels; what Image::Load feeds to
+    // the gamma step); imagebytes: the texels of scene::Image (stbi_loadf + FloatToByte).
+    // Output: int32 width, int32 height, then width * height * 3 bytes (0 x 0 on failure).
+    int32_t wh[2] = {0, 0};
+    std::vector<unsigned char> bytes;
+    if (cmd == "image8") {
+      int n = 0;
+      unsigned char* d = stbi_load(argv[2], &wh[0], &wh[1], &n, 3);
+      if (d) bytes.assign(d, d + (size_t)wh[0] * wh[1] * 3), stbi_image_free(d);
+      else wh[0] = wh[1] = 0;
+    } else {
+      scene::Image img(argv[2]);
+      wh[0] = img.Width(), wh[1] = img.Height();
+      if (img.Height() <= 0) wh[0] = wh[1] = 0;
+      for (int y = 0; y < wh[1]; y++)
+        for (int x = 0; x < wh[0]; x++) bytes.insert(bytes.end(), img.PixelData(x, y), img.PixelData(x, y) + 3);
+    }
+    std::ofstream o(argv[3], std::ios::binary);
+    o.write((const char*)wh, sizeof wh);
+    o.write((const char*)bytes.data(), (std::streamsize)bytes.size());
   } else if (cmd == "texels" && argc == 3) {
     scene::Image img("earthmap.jpg");
     std::ofstream o(argv[2], std::ios::binary);

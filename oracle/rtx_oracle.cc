@@ -1080,6 +1080,21 @@ bool load_obj(const std::string& path, double scale, int mat, std::vector<Prim>&
   return true;
 }
 
+std::vector<std::string> split_dirs(const char* list) {
+  std::vector<std::string> out;
+  std::string cur;
+  for (const char* c = list; *c; c++) {
+    if (*c == ':') {
+      if (!cur.empty()) out.push_back(cur);
+      cur.clear();
+    } else {
+      cur += *c;
+    }
+  }
+  if (!cur.empty()) out.push_back(cur);
+  return out;
+}
+
 Scene* load_scene(const char* file, const char* asset_dir, std::string& err) {
   std::ifstream in(file);
   if (!in) {
@@ -1114,7 +1129,12 @@ Scene* load_scene(const char* file, const char* asset_dir, std::string& err) {
         ss >> name;
         T.kind = TEX_IMAGE;
         T.img = std::make_shared<Image>();
-        if (!load_ppm(std::string(asset_dir) + "/" + name + ".ppm", *T.img)) T.img->w = T.img->h = 0;
+        // texels of the reference's decode (the fixture tests/golden/textures/<name>.ppm):
+        // asset_dir may list several directories separated by ':'
+        bool ok = false;
+        for (const std::string& dir : split_dirs(asset_dir))
+          if ((ok = load_ppm(dir + "/" + name + ".ppm", *T.img))) break;
+        if (!ok) T.img->w = T.img->h = 0;
       }
       S->tex.push_back(T);
     } else if (kw == "mat") {
@@ -1151,7 +1171,10 @@ Scene* load_scene(const char* file, const char* asset_dir, std::string& err) {
       double sc;
       int m;
       ss >> name >> sc >> m;
-      if (!load_obj(std::string(asset_dir) + "/" + name, sc, m, S->prims)) {
+      bool ok = false;
+      for (const std::string& dir : split_dirs(asset_dir))
+        if ((ok = load_obj(dir + "/" + name, sc, m, S->prims))) break;
+      if (!ok) {
         err = "cannot open obj " + name;
         return nullptr;
       }
