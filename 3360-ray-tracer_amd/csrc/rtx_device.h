@@ -1525,14 +1525,27 @@ struct ShadeOut {
   V3 f;
   float ct, pdf;
   int32_t what;
+  int32_t fsrc;  // DEFER_F: 1 f = albedo / pi (Lambertian), 2 f = albedo (Metal), read by shade_finish
 };
+// A copy of a pointer the compiler cannot see through: loads through it are issued where they
+// are written (late), not hoisted to an earlier load of the same address and kept live.
+template <class T>
+__device__ __forceinline__ const T* opaque(const T* p) {
+  asm volatile("" : "+v"(p));
+  return p;
+}
 
 // SET_ORIGIN = false: a continuing path's new origin (the hit point) is left for the caller
 // to set, so a caller that parked the hit point elsewhere keeps rec.p out of registers.
-template <bool LAMB = false, bool NOTEX = false, bool SET_ORIGIN = true>
+// DEFER_F (texture-free builds): the BSDF value of a Lambertian / Metal hit is the material's
+// albedo (/ pi); it is read from the material table by shade_finish, at the end, instead of
+// being held in registers across the direction sampling.
+template <bool LAMB = false, bool NOTEX = false, bool SET_ORIGIN = true, bool DEFER_F = false>
 __device__ __forceinline__ void shade_core(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit, Rng& g,
                                            const rtx_material& m, ShadeOut& so) {
+  static_assert(!DEFER_F || NOTEX, "deferred BSDF values need texture-free shading");
   so.what = kShadeDead;
+  so.fsrc = 0;
   double lnd;
   const V3 nd = normalize_l(p.d, lnd);  // wo = -nd (hit), sky(d) (miss)
   if (!hit || p.depth >= max_depth) {
@@ -1621,7 +1634,8 @@ __device__ __forceinline__ void shade_core(const DScene& S, int max_depth, Path&
     if (dot(wi, n) <= 0) return;
     const float cf = (float)dot(n, wi);
     const float pdf = (cf <= 0.0f) ? 0.0f : (float)((double)cf / kPi);
-    so.f = mat_tex_t<NOTEX>(S, m, rec) / kPi;
+    if (DEFER_F) so.fsrc = 1;
+    else so.f = mat_tex_t<NOTEX>(S, m, rec) / kPi;
     if (pdf < 1e-6f) return;
     so.ct = fmaxf(0.0f, (float)dot(wi, n));
     so.pdf = pdf;
@@ -1629,7 +1643,8 @@ __device__ __forceinline__ void shade_core(const DScene& S, int max_depth, Path&
   } else if (isM) {
     wi = s4;
     if (dot(wi, n) <= 0) return;
-    so.f = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
+    if (DEFER_F) so.fsrc = 2;
+    else so.f = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
     so.what = kShadeSpecular;
   } else {
     if (g_reflect) {
@@ -1649,14 +1664,21 @@ __device__ __forceinline__ void shade_core(const DScene& S, int max_depth, Path&
 
 // The rest of the step: radiance of a terminated path, or the child's throughput and Russian
 // roulette (wavefront.cc:189-205) with the segment's last draw.  depth = the child's depth.
-__device__ __forceinline__ bool shade_finish(const ShadeOut& so, V3& thr, int32_t depth, Rng& g, V3& L) {
+__device__ __forceinline__ bool shade_finish(const ShadeOut& so, V3& thr, int32_t depth, Rng& g, V3& L,
+                                             const rtx_material* m = nullptr) {
   L = v3(0, 0, 0);
   if (so.what == kShadeEmit) {
     L = L + thr * so.f;
     return false;
   }
   if (so.what == kShadeDead) return false;
-  V3 c = so.what == kShadeDiffuse ? ((double)so.ct * (thr * so.f)) / (double)so.pdf : thr * so.f;
+  V3 f = so.f;
+  if (so.fsrc) {  // DEFER_F: the texture-free BSDF value, read now (shade_core)
+    const rtx_material* mp = opaque(m);
+    f = v3(mp->albedo[0], mp->albedo[1], mp->albedo[2]);
+    if (so.fsrc == 1) f = f / kPi;
+  }
+  V3 c = so.what == kShadeDiffuse ? ((double)so.ct * (thr * f)) / (double)so.pdf : thr * f;
   if (depth > 5) {
     double q = fmax(fmax(c.x, c.y), c.z);
     q = q < 0.1 ? 0.1 : (q > 0.95 ? 0.95 : q);

@@ -125,6 +125,12 @@ constexpr size_t stack_lds_bytes(int STACK) { return (size_t)(STACK + 1) * kBloc
 #ifndef RTX_THR_LDS
 #define RTX_THR_LDS 1  // persistent: path throughput parked in LDS across the traversal (no VGPR spill of it)
 #endif
+#ifndef RTX_LAZY_MAT
+#define RTX_LAZY_MAT 1  // persistent (merged shading): material fields read at their use
+#endif
+#ifndef RTX_DEFER_F
+#define RTX_DEFER_F 0  // persistent, texture-free builds: the BSDF albedo read at the end of shading (no gain over RTX_LAZY_MAT)
+#endif
 #ifndef RTX_HITP_LDS
 #define RTX_HITP_LDS 1  // persistent, texture-free builds: the hit point parked in LDS across the BSDF sampling
 #endif
@@ -506,9 +512,17 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
         // the throughput is read from LDS only after the shading core: none of its registers
         // are live across the walk or the BSDF sampling
         ShadeOut so;
-        shade_core<LAMB, NOTEX, !kHitpLds>(A.S, A.max_depth, P, h, best >= 0, g, m, so);
+        constexpr bool kDeferF = NOTEX && RTX_DEFER_F;
+#if RTX_LAZY_MAT
+        // the material's fields are read where shading uses them (a reference into the table,
+        // not a copy loaded up front and held across the sampling)
+        const rtx_material& mr = *opaque(A.S.mats + (best >= 0 ? h.mat : 0));
+        shade_core<LAMB, NOTEX, !kHitpLds, kDeferF>(A.S, A.max_depth, P, h, best >= 0, g, mr, so);
+#else
+        shade_core<LAMB, NOTEX, !kHitpLds, kDeferF>(A.S, A.max_depth, P, h, best >= 0, g, m, so);
+#endif
         V3 thr = v3(thr_lds[0], thr_lds[kBlock], thr_lds[2 * kBlock]);
-        cont = shade_finish(so, thr, P.depth, g, L);
+        cont = shade_finish(so, thr, P.depth, g, L, best >= 0 ? A.S.mats + h.mat : A.S.mats);
         if (cont) thr_lds[0] = thr.x, thr_lds[kBlock] = thr.y, thr_lds[2 * kBlock] = thr.z;
         if (kHitpLds && cont) P.o = v3(hitp_lds[0], hitp_lds[kBlock], hitp_lds[2 * kBlock]);
 #else
