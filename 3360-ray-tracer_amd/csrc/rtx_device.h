@@ -159,13 +159,83 @@ __device__ __forceinline__ V3 random_in_unit_disk(Rng& g) {  // math_utils.h:83-
     if (len2(p) < 1.0) return p;
   }
 }
+// cos(phi) and sin(phi) for 0 <= phi < 2^30 with ONE shared argument reduction, bit for bit
+// what the device library's cos() and sin() return there: the same operations as its
+// small-argument reduction (x * 2/pi rounded to an integer quadrant, pi/2 in three parts
+// with exact error terms) and its sincos kernel polynomials, then the quadrant selection and
+// sign rules of cos() / sin().  The library's large-argument (Payne-Hanek) path, which the
+// Lambertian angle 2*pi*r1 < 2*pi never takes, is not compiled in: its registers made the
+// shading spill.  -ffp-contract=off keeps every product and sum separately rounded, as in
+// the library; fma() is the library's fma.
+//   RTX_SINCOS_SMALL 0: the library's cos() and sin(); 1: both from one shared reduction;
+//   2: cos and sin each from its own small-argument reduction (fewest live registers: the
+//   plain kernel's texture-free builds lose their last spills, A/B r02 `ab_sincos2_*`).
+// Register allocation decides which is best per kernel, so the PARK TU picks its own value.
+#ifndef RTX_SINCOS_SMALL
+#define RTX_SINCOS_SMALL 2
+#endif
+__device__ __forceinline__ void sincos_small(double x, double& sn, double& cs) {
+  // reduction: x = q * pi/2 + (hi + lo)
+  const double q = rint(x * 0x1.45f306dc9c883p-1);
+  const double c1 = 0x1.1a62633145c00p-54;
+  const double t4 = fma(q, -0x1.921fb54442d18p+0, x);
+  const double t5 = fma(q, -c1, t4);
+  const double t6 = q * c1;
+  const double t8 = fma(q, c1, -t6);
+  const double t9 = t4 - t6;
+  const double t11 = (t4 - t9) - t6;
+  const double t14 = ((t9 - t5) + t11) - t8;
+  const double t15 = fma(q, -0x1.b839a252049c0p-104, t14);
+  const double hi = t5 + t15;
+  const double lo = t15 - (hi - t5);
+  const int quad = (int)q & 3;
+  // kernel on [-pi/4, pi/4]
+  const double x2 = hi * hi;
+  const double h = x2 * 0.5;
+  const double w = 1.0 - h;
+  const double e = (1.0 - w) - h;
+  const double x4 = x2 * x2;
+  double pc = fma(x2, -0x1.907db46cc5e42p-37, 0x1.1eeb69037ab78p-29);
+  pc = fma(x2, pc, -0x1.27e4fa17f65f6p-22);
+  pc = fma(x2, pc, 0x1.a01a019f4ec90p-16);
+  pc = fma(x2, pc, -0x1.6c16c16c16967p-10);
+  pc = fma(x2, pc, 0x1.5555555555555p-5);
+  const double kc = w + fma(x4, pc, fma(hi, -lo, e));
+  double ps = fma(x2, 0x1.5e0b2f9a43bb8p-33, -0x1.ae600b42fdfa7p-26);
+  ps = fma(x2, ps, 0x1.71de3796cde01p-19);
+  ps = fma(x2, ps, -0x1.a01a019e83e5cp-13);
+  ps = fma(x2, ps, 0x1.1111111110bb3p-7);
+  const double hx3 = hi * -x2;
+  const double ks = hi - fma(hx3, -0x1.5555555555555p-3, fma(x2, fma(hx3, ps, lo * 0.5), -lo));
+  // quadrant: cos = (c, -s, -c, s), sin = (s, c, -s, -c) (x >= +0: no sign from x)
+  const double c0 = (quad & 1) == 0 ? kc : -ks;
+  const double s0 = (quad & 1) == 0 ? ks : kc;
+  cs = quad > 1 ? -c0 : c0;
+  sn = quad > 1 ? -s0 : s0;
+}
+__device__ __forceinline__ void cos_sin(double phi, double& c, double& s) {
+#if RTX_SINCOS_SMALL == 2
+  double t;
+  sincos_small(phi, t, c);
+  asm volatile("" : "+v"(c));
+  asm volatile("" : "+v"(phi));
+  sincos_small(phi, s, t);
+#elif RTX_SINCOS_SMALL
+  sincos_small(phi, s, c);
+#else
+  c = cos(phi), s = sin(phi);
+#endif
+}
+
 __device__ __forceinline__ V3 random_cosine_direction(Rng& g, V3 normal) {  // math_utils.h:104-123
   double r1 = g.next();
   double r2 = g.next();
   double phi = 2.0 * kPi * r1;
   double r = sqrt(r2);
-  double x = r * cos(phi);
-  double y = r * sin(phi);
+  double cph, sph;
+  cos_sin(phi, cph, sph);
+  double x = r * cph;
+  double y = r * sph;
   double z = sqrt(1.0 - r2);
   V3 w = normalize(normal);
   V3 a = (fabs(w.x) > 0.9) ? v3(0, 1, 0) : v3(1, 0, 0);
@@ -1590,8 +1660,10 @@ __device__ __forceinline__ void shade_core(const DScene& S, int max_depth, Path&
   double x = 0.0, y = 0.0;
   if (isL) {
     const double phi = 2.0 * kPi * r1;
-    x = s2 * cos(phi);
-    y = s2 * sin(phi);
+    double cph, sph;
+    cos_sin(phi, cph, sph);
+    x = s2 * cph;
+    y = s2 * sph;
   }
   bool g_reflect = false;
   V3 perp = v3(0, 0, 0);

@@ -2,6 +2,11 @@
 // true>), compiled apart from rtx_capi.hip so this translation unit can use the LLVM
 // max-memory-clause scheduler (see the Makefile and rtx_kernels.h).
 #define RTX_PERSISTENT_ONLY 1
+// the library cos()/sin() here: with the small-argument form the bunny's triangle-tree
+// Lambertian build spills (0 -> 56 B per lane), see rtx_device.h
+#ifndef RTX_SINCOS_SMALL
+#define RTX_SINCOS_SMALL 0
+#endif
 #include <hip/hip_runtime.h>
 
 #include "rtx.h"
