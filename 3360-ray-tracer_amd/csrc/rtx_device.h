@@ -355,6 +355,15 @@ __device__ __forceinline__ bool hit_sphere(const double* g, int32_t mat, V3 o, V
 #ifndef RTX_TRI_EDGES
 #define RTX_TRI_EDGES 1
 #endif
+#ifndef RTX_TRI_BRANCHLESS
+#define RTX_TRI_BRANCHLESS 0  // traversal's triangle test without early exits (prim_t); the PARK TU sets 1 (A/B r02: bunny +3.8 %, C5 plain kernel -1.9 %)
+#endif
+#ifndef RTX_KIND_UNPINNED
+#define RTX_KIND_UNPINNED 1  // kind-specialised primitive tests do not load the kind word (A/B r02: bunny +0.3 %, C5 +0.3 %)
+#endif
+#ifndef RTX_SPH_BRANCHLESS
+#define RTX_SPH_BRANCHLESS 0  // traversal's sphere test: 1 no early exits, 2 only the far root conditional (A/B r02: -2.5 % / +-0 C2)
+#endif
 __device__ __forceinline__ V3 tri_e1(const double* g) {
   if (RTX_TRI_EDGES) return V3{g[3], g[4], g[5]};
   return V3{g[3], g[4], g[5]} - V3{g[0], g[1], g[2]};
@@ -446,6 +455,7 @@ struct PrimRec {
   int32_t mat;
   double g[9];
 };
+template <bool KIND_KNOWN = false>
 __device__ __forceinline__ PrimRec load_prim(const rtx_prim* __restrict__ P, bool tris) {
   PrimRec r;
 #if RTX_PRIM_PRELOAD
@@ -454,8 +464,10 @@ __device__ __forceinline__ PrimRec load_prim(const rtx_prim* __restrict__ P, boo
   const double2 w1 = *((const double2*)P + 1), w2 = *((const double2*)P + 2);
   double2 w3 = make_double2(0.0, 0.0), w4 = make_double2(0.0, 0.0);
   if (tris) w3 = *((const double2*)P + 3), w4 = *((const double2*)P + 4);
-  asm volatile("" ::"v"(w0.x), "v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w2.x), "v"(w2.y), "v"(w3.x),
-               "v"(w3.y), "v"(w4.x), "v"(w4.y));
+  // (a kind-specialised caller never reads the kind word: it is not pinned, so not loaded)
+  if (!(RTX_KIND_UNPINNED && KIND_KNOWN)) asm volatile("" ::"v"(w0.x));
+  asm volatile("" ::"v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w2.x), "v"(w2.y), "v"(w3.x), "v"(w3.y),
+               "v"(w4.x), "v"(w4.y));
   r.kind = (int)w0.x;
   r.mat = (int32_t)w0.y;
   r.g[0] = __hiloint2double((int)w0.w, (int)w0.z);
@@ -475,10 +487,29 @@ __device__ __forceinline__ PrimRec load_prim(const rtx_prim* __restrict__ P, boo
 template <int KIND = -1>
 __device__ __forceinline__ bool prim_t(const rtx_prim* __restrict__ Pp, bool tris, V3 o, V3 d, double tmin,
                                        double tmax, double& t_out, int32_t& mat_out) {
-  const PrimRec R = load_prim(Pp, KIND < 0 ? tris : KIND == (int)RTX_PRIM_TRIANGLE);
+  const PrimRec R = load_prim<(KIND >= 0)>(Pp, KIND < 0 ? tris : KIND == (int)RTX_PRIM_TRIANGLE);
   mat_out = R.mat;
   const PrimRec* P = &R;
   const int kind = KIND >= 0 ? KIND : P->kind;
+  if (RTX_TRI_BRANCHLESS && kind == RTX_PRIM_TRIANGLE) {
+    // the same operations without the early exits: every value is computed and the four
+    // rejections are combined at the end (a wave's few active leaf lanes rarely all take
+    // the same early exit, so the branches only add mask bookkeeping)
+    const V3 A{P->g[0], P->g[1], P->g[2]};
+    const V3 e1 = tri_e1(P->g), e2 = tri_e2(P->g);
+    const V3 pvec = cross(d, e2);
+    const float det = (float)dot(e1, pvec);
+    const float inv_det = 1.0f / det;
+    const V3 tvec = o - A;
+    const float u = (float)(dot(tvec, pvec) * (double)inv_det);
+    const V3 qvec = cross(tvec, e1);
+    const float v = (float)(dot(d, qvec) * (double)inv_det);
+    const float t = (float)(dot(e2, qvec) * (double)inv_det);
+    const bool ok = !(fabsf(det) < 1e-6f) & !(u < 0.0f || u > 1.0f) & !(v < 0.0f || (u + v) > 1.0f) &
+                    !((double)t < tmin || (double)t > tmax);
+    t_out = (double)t;
+    return ok;
+  }
   if (kind == RTX_PRIM_TRIANGLE) {
     V3 A{P->g[0], P->g[1], P->g[2]};
     V3 e1 = tri_e1(P->g), e2 = tri_e2(P->g);
@@ -505,9 +536,17 @@ __device__ __forceinline__ bool prim_t(const rtx_prim* __restrict__ Pp, bool tri
     double h = dot(d, oc);
     double cc = len2(oc) - radius * radius;
     double disc = h * h - a * cc;
-    if (disc < 0) return false;
+    if (RTX_SPH_BRANCHLESS == 1) {  // both roots, no early exit (sqrt of disc < 0 is NaN: both fail)
+      const double sq = sqrt(disc);
+      const double r1 = (h - sq) / a, r2 = (h + sq) / a;
+      const bool ok1 = tmin < r1 && r1 < tmax, ok2 = tmin < r2 && r2 < tmax;
+      t_out = ok1 ? r1 : r2;
+      return !(disc < 0) & (ok1 | ok2);
+    }
+    if (!RTX_SPH_BRANCHLESS && disc < 0) return false;
     double sq = sqrt(disc);
     double root = (h - sq) / a;
+    if (RTX_SPH_BRANCHLESS && disc < 0) return false;
     if (!(tmin < root && root < tmax)) {
       root = (h + sq) / a;
       if (!(tmin < root && root < tmax)) return false;

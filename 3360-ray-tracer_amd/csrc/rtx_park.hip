@@ -7,6 +7,11 @@
 #ifndef RTX_SINCOS_SMALL
 #define RTX_SINCOS_SMALL 0
 #endif
+// ... and the triangle test without early exits (bunny +3.8 %; the plain kernel's builds are
+// slower with it)
+#ifndef RTX_TRI_BRANCHLESS
+#define RTX_TRI_BRANCHLESS 1
+#endif
 #include <hip/hip_runtime.h>
 
 #include "rtx.h"
