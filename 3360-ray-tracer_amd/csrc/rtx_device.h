@@ -358,6 +358,9 @@ __device__ __forceinline__ bool hit_sphere(const double* g, int32_t mat, V3 o, V
 #ifndef RTX_TRI_BRANCHLESS
 #define RTX_TRI_BRANCHLESS 0  // traversal's triangle test without early exits (prim_t); the PARK TU sets 1 (A/B r02: bunny +3.8 %, C5 plain kernel -1.9 %)
 #endif
+#ifndef RTX_EARLY_TEX
+#define RTX_EARLY_TEX 1  // textured builds: Lambertian albedo texture looked up before the sampling (shade_core; A/B r02: C5 +0.3 %)
+#endif
 #ifndef RTX_KIND_UNPINNED
 #define RTX_KIND_UNPINNED 1  // kind-specialised primitive tests do not load the kind word (A/B r02: bunny +0.3 %, C5 +0.3 %)
 #endif
@@ -1055,6 +1058,9 @@ __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, doub
 #ifndef RTX_PUSH_BRANCHLESS
 #define RTX_PUSH_BRANCHLESS 1  // lean walk: unconditional child stores, sp advanced per entered child
 #endif
+#ifndef RTX_POP_BRANCHLESS
+#define RTX_POP_BRANCHLESS 0  // lean walk: stack pop without a branch (read below sp, select)
+#endif
 #ifndef RTX_PK_SLAB
 #define RTX_PK_SLAB 0  // lean walk: slab plane distances with packed f32 FMAs (A/B r02: bit-identical, -2.6 % C2, -3.9 % bunny, -5.8 % C5; off)
 #endif
@@ -1326,6 +1332,24 @@ __device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double t
     cswap4(tt[0], cc[0], tt[2], cc[2]);
     cswap4(tt[1], cc[1], tt[3], cc[3]);
     cswap4(tt[1], cc[1], tt[2], cc[2]);
+#if RTX_PUSH_BRANCHLESS && RTX_POP_BRANCHLESS
+    // push and pop without a branch: the pushes are stored and counted as below (a visit
+    // that enters no child advances sp by nothing, its stores land just above the top), then
+    // every lane reads the slot below sp and keeps it only when it entered nothing
+    {
+      const bool enter = tt[0] != __builtin_inff();
+#pragma unroll
+      for (int c = 3; c >= 1; c--) {
+        stk[sp * stride] = (uint32_t)cc[c];
+        sp += tt[c] != __builtin_inff() ? 1 : 0;
+      }
+      if (!enter && sp == 0) break;
+      const uint32_t top = stk[(sp > 0 ? sp - 1 : 0) * stride];
+      node = enter ? (uint32_t)cc[0] : top;
+      sp -= enter ? 0 : 1;
+      continue;
+    }
+#endif
     if (tt[0] != __builtin_inff()) {
 #if RTX_PUSH_BRANCHLESS
       // The sort leaves the entered children as a prefix (the others carry +inf and sort
@@ -1393,10 +1417,21 @@ __device__ __forceinline__ int64_t trace_fast4_lean(const DScene& S, V3 o, V3 d,
 // Textures / materials
 // ---------------------------------------------------------------------------------------
 // Deferred get_sphere_uv for image textures: outward = (p - c) / r exactly as hit_sphere.
-__device__ __noinline__ void lazy_sphere_uv(const rtx_prim* __restrict__ P, V3 p, double& u, double& v) {
+// (Returned by value: reference outputs of a call live in scratch memory.)
+#ifndef RTX_LAZY_UV_INLINE
+#define RTX_LAZY_UV_INLINE 0  // 1: inlined instead of called
+#endif
+#if RTX_LAZY_UV_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+double2 lazy_sphere_uv(const rtx_prim* __restrict__ P, V3 p) {
   V3 c{P->g[0], P->g[1], P->g[2]};
   double radius = fmax(0.0, P->g[3]);
-  sphere_uv((p - c) / radius, u, v);
+  double2 uv;
+  sphere_uv((p - c) / radius, uv.x, uv.y);
+  return uv;
 }
 
 __device__ __forceinline__ V3 tex_value(const DScene& S, int32_t t, const Hit& rec) {
@@ -1416,7 +1451,10 @@ __device__ __forceinline__ V3 tex_value(const DScene& S, int32_t t, const Hit& r
     if (T.image < 0) return v3(0, 1, 1);
     const DImage im = S.images[T.image];
     if (im.h <= 0) return v3(0, 1, 1);
-    if (rec.lazy_sphere >= 0) lazy_sphere_uv(S.prims + rec.lazy_sphere, p, u, v);
+    if (rec.lazy_sphere >= 0) {
+      const double2 uv = lazy_sphere_uv(S.prims + rec.lazy_sphere, p);
+      u = uv.x, v = uv.y;
+    }
     u = u < 0 ? 0 : (u > 1 ? 1 : u);
     v = 1.0 - (v < 0 ? 0 : (v > 1 ? 1 : v));
     int i = (int)(u * im.w);
@@ -1675,6 +1713,11 @@ __device__ __forceinline__ void shade_core(const DScene& S, int max_depth, Path&
   const bool isL = kind == RTX_MAT_LAMBERTIAN, isM = kind == RTX_MAT_METAL, isG = kind == RTX_MAT_DIELECTRIC;
   if (!(isL || isM || isG)) return;  // DiffuseLight::Sample
   const V3 n = rec.normal;
+  // EARLY_TEX (textured builds): a Lambertian's albedo texture is looked up here, before the
+  // direction sampling, so the hit point / u,v / lazy-uv sphere are dead during the sampling
+  // (only the colour is kept); the same lookup, only earlier
+  V3 ftex = v3(0, 0, 0);
+  if (RTX_EARLY_TEX && !NOTEX && !DEFER_F && isL) ftex = mat_tex_t<NOTEX>(S, m, rec);
   double r1 = 0.0, r2 = 0.0;
   if (isL) r1 = g.next(), r2 = g.next();
   V3 ru = v3(0, 0, 0);
@@ -1746,7 +1789,7 @@ __device__ __forceinline__ void shade_core(const DScene& S, int max_depth, Path&
     const float cf = (float)dot(n, wi);
     const float pdf = (cf <= 0.0f) ? 0.0f : (float)((double)cf / kPi);
     if (DEFER_F) so.fsrc = 1;
-    else so.f = mat_tex_t<NOTEX>(S, m, rec) / kPi;
+    else so.f = ((RTX_EARLY_TEX && !NOTEX) ? ftex : mat_tex_t<NOTEX>(S, m, rec)) / kPi;
     if (pdf < 1e-6f) return;
     so.ct = fmaxf(0.0f, (float)dot(wi, n));
     so.pdf = pdf;

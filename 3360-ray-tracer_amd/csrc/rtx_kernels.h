@@ -346,7 +346,8 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
   uint32_t* stk = lds + threadIdx.x;
   double* thr_lds = (double*)(lds + A.stack_slots * kBlock) + threadIdx.x;  // [c * kBlock] (RTX_THR_LDS)
   double* hitp_lds = thr_lds + kLdsThr * kBlock;                             // [c * kBlock] (RTX_HITP_LDS)
-  constexpr bool kHitpLds = RTX_HITP_LDS && NOTEX && !SCATTER && RTX_MERGED_SHADE;  // nothing else reads rec.p
+  // nothing else reads rec.p (textured builds: once the texture lookups moved before the sampling)
+  constexpr bool kHitpLds = RTX_HITP_LDS && (NOTEX || RTX_EARLY_TEX) && !SCATTER && RTX_MERGED_SHADE;
   (void)hitp_lds;
   // this wave's pooled-leaf-test list (after the throughput and hit-point areas)
   uint32_t* pool = (FAST && RTX_LEAF_POOL && A.S.pool_ok)
