@@ -356,7 +356,7 @@ __device__ __forceinline__ bool hit_sphere(const double* g, int32_t mat, V3 o, V
 #define RTX_TRI_EDGES 1
 #endif
 #ifndef RTX_TRI_BRANCHLESS
-#define RTX_TRI_BRANCHLESS 0  // traversal's triangle test without early exits (prim_t); the PARK TU sets 1 (A/B r02: bunny +3.8 %, C5 plain kernel -1.9 %)
+#define RTX_TRI_BRANCHLESS 0  // traversal's triangle test without early exits (prim_t): 1 in kind-specialised tests, 2 in all; the PARK TU sets 1 (A/B r02: bunny +3.8 %, C5 plain kernel -1.9 %)
 #endif
 #ifndef RTX_EARLY_TEX
 #define RTX_EARLY_TEX 1  // textured builds: Lambertian albedo texture looked up before the sampling (shade_core; A/B r02: C5 +0.3 %)
@@ -494,7 +494,7 @@ __device__ __forceinline__ bool prim_t(const rtx_prim* __restrict__ Pp, bool tri
   mat_out = R.mat;
   const PrimRec* P = &R;
   const int kind = KIND >= 0 ? KIND : P->kind;
-  if (RTX_TRI_BRANCHLESS && kind == RTX_PRIM_TRIANGLE) {
+  if (RTX_TRI_BRANCHLESS && (RTX_TRI_BRANCHLESS == 2 || KIND >= 0) && kind == RTX_PRIM_TRIANGLE) {
     // the same operations without the early exits: every value is computed and the four
     // rejections are combined at the end (a wave's few active leaf lanes rarely all take
     // the same early exit, so the branches only add mask bookkeeping)

@@ -12,6 +12,11 @@
 #ifndef RTX_TRI_BRANCHLESS
 #define RTX_TRI_BRANCHLESS 1
 #endif
+// ... and the texture lookup where the reference does it: the early lookup makes the generic
+// (textured) PARK build spill more (80 -> 128 B per lane)
+#ifndef RTX_EARLY_TEX
+#define RTX_EARLY_TEX 0
+#endif
 #include <hip/hip_runtime.h>
 
 #include "rtx.h"
