@@ -1373,6 +1373,62 @@ int rtx_write_ppm(const char* path, const double* rgb, int32_t w, int32_t h) {
 
 }  // extern "C"
 
+// ---------------------------------------------------------------------------------------
+// Self-check of the restated small-argument cos/sin (rtxd::sincos_small, used by the plain
+// kernel's Lambertian sampling) against the device library's cos() and sin(): n arguments
+// phi = 2*pi*u with u the reference's 53-bit uniform draws (a 64-bit mix of seed and index,
+// top 53 bits), plus the ends of [0, 1) and the quadrant boundaries.  Test hook only (not in
+// rtx.h): tests/test_gpu_timed.py.
+namespace {
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__global__ void k_check_sincos(int64_t n, uint64_t seed, unsigned long long* bad, double* first_bad) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n + 64; i += (int64_t)gridDim.x * blockDim.x) {
+    double u;
+    if (i < n) {
+      u = (double)(mix64(seed + (uint64_t)i) >> 11) * 0x1.0p-53;
+    } else {  // 0, the largest draw, and 1/4, 1/2, 3/4 (and their neighbours)
+      const int j = (int)(i - n);
+      const double base[5] = {0.0, 1.0, 0.25, 0.5, 0.75};
+      u = base[j % 5];
+      const int steps = j / 5 - 6;  // -6 .. +6 draws around the point
+      u += steps * 0x1.0p-53;
+      if (u < 0.0 || u >= 1.0) continue;
+    }
+    const double phi = 2.0 * rtxd::kPi * u;
+    double s, c;
+    rtxd::sincos_small(phi, s, c);
+    const double c0 = cos(phi), s0 = sin(phi);
+    if (__double_as_longlong(c) != __double_as_longlong(c0) || __double_as_longlong(s) != __double_as_longlong(s0)) {
+      if (atomicAdd(bad, 1ull) == 0) *first_bad = u;
+    }
+  }
+}
+}  // namespace
+
+extern "C" int rtx_internal_check_sincos(int device, int64_t n, uint64_t seed, int64_t* mismatches,
+                                         double* first_bad) {
+  if (n < 0 || !mismatches) return fail(RTX_ERR_INVALID, "bad argument");
+  HIPC(hipSetDevice(device));
+  struct Owned : DevBuf {
+    ~Owned() { release(); }
+  } b;
+  int rc;
+  if ((rc = b.reserve(2 * sizeof(unsigned long long)))) return rc;
+  HIPC(hipMemset(b.p, 0, 2 * sizeof(unsigned long long)));
+  unsigned long long* bad = b.as<unsigned long long>();
+  hipLaunchKernelGGL(k_check_sincos, dim3(1024), dim3(256), 0, nullptr, n, seed, bad, (double*)(bad + 1));
+  HIPC(hipGetLastError());
+  unsigned long long h[2];
+  HIPC(hipMemcpy(h, bad, sizeof(h), hipMemcpyDeviceToHost));
+  *mismatches = (int64_t)h[0];
+  if (first_bad) std::memcpy(first_bad, &h[1], sizeof(double));
+  return RTX_OK;
+}
+
 namespace {
 
 // Which persistent fast schedule suits this scene: the PARK kernel wins where a few lanes

@@ -269,3 +269,20 @@ def test_schedule_timing_is_ordered_after_user_stream_work(rtx_mod, scenes):
     s.synchronize()
     assert np.array_equal(a.cpu().numpy(), want_a)
     assert np.array_equal(b.cpu().numpy(), want_b)
+
+
+def test_restated_sincos_is_the_library_bit_for_bit(rtx_mod, gpu):
+    """The plain kernel's Lambertian cos/sin of 2*pi*r1 come from a restatement of the device
+    library's small-argument path (rtx_device.h sincos_small, one reduction each, no
+    Payne-Hanek branch): on 2^24 random draws r1 (the reference's 53-bit uniforms) and around
+    0, 1/4, 1/2, 3/4 and the largest draw, both must equal the library's cos() and sin() bit
+    for bit."""
+    import ctypes as C
+
+    f = rtx_mod.lib().rtx_internal_check_sincos
+    f.argtypes = [C.c_int, C.c_int64, C.c_uint64, C.POINTER(C.c_int64), C.POINTER(C.c_double)]
+    f.restype = C.c_int
+    bad, first = C.c_int64(-1), C.c_double(0.0)
+    for seed in (1, 0x5EED):
+        assert f(0, 1 << 24, seed, C.byref(bad), C.byref(first)) == 0, rtx_mod.lib().rtx_last_error()
+        assert bad.value == 0, f"{bad.value} mismatches, first at u = {first.value!r}"
