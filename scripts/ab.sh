@@ -13,7 +13,7 @@ for round in 1 2; do
   for lib in "$@"; do
     if [ "$lib" = "default" ]; then L=""; else L="$R/$lib"; fi
     res=$(RTX_LIB=$L timeout -k 10 300 python bench.py --no-cpu-baseline $ARGS 2>>gpurun_out/ab_$TAG.err) || exit $?
-    echo "round $round $lib $(echo "$res" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); r=d["roofline"]; print("%.1f Mrays/s ms/step %.2f frac %s" % (d["value"], d["ms_per_step"], r.get("frac")))')" >> $OUT
+    echo "round $round $lib $(echo "$res" | python3 -c 'import json,sys; d=json.loads(sys.stdin.read().strip().splitlines()[-1]); r=d["roofline"]; print("%.1f Mrays/s ms/step %.2f frac %s nodes/seg %.3f prims/seg %.3f" % (d["value"], d["ms_per_step"], r.get("frac"), r.get("nodes_per_segment", 0), r.get("prims_per_segment", 0)))')" >> $OUT
   done
 done
 cat $OUT
