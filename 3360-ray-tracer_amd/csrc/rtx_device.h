@@ -304,10 +304,10 @@ struct Hit {  // HitRecord (hittable.h:18-42)
   double t, u, v;
   int32_t mat;
   int32_t front_face;
-  // Sphere u,v (acos/atan2, sphere.h:73-79) are only ever read by image textures, so the
-  // shading path defers them: lazy_sphere >= 0 names the sphere whose u,v are still to be
-  // derived from p (same arithmetic as at hit time, hence the same values).
-  int64_t lazy_sphere;
+  // Sphere u,v (acos/atan2, sphere.h:73-79) and rect u,v (rect.h) are only ever read by image
+  // textures, so the shading path defers them: lazy_uv >= 0 names the primitive whose u,v
+  // are still to be derived from p (same arithmetic as at hit time, hence the same values).
+  int64_t lazy_uv;
 };
 
 __device__ __forceinline__ void set_face_normal(Hit& h, V3 d, V3 outward) {  // hittable.h:31-34
@@ -360,6 +360,9 @@ __device__ __forceinline__ bool hit_sphere(const double* g, int32_t mat, V3 o, V
 #endif
 #ifndef RTX_EARLY_TEX
 #define RTX_EARLY_TEX 1  // textured builds: Lambertian albedo texture looked up before the sampling (shade_core; A/B r02: C5 +0.3 %)
+#endif
+#ifndef RTX_LAZY_RECT_UV
+#define RTX_LAZY_RECT_UV 1  // persistent shading: rect u,v derived from p at the image-texture lookup (like a sphere's)
 #endif
 #ifndef RTX_KIND_UNPINNED
 #define RTX_KIND_UNPINNED 1  // kind-specialised primitive tests do not load the kind word (A/B r02: bunny +0.3 %, C5 +0.3 %)
@@ -582,7 +585,7 @@ template <bool UV = true>
 __device__ __forceinline__ void finish_hit(const DScene& S, int64_t best, V3 o, V3 d, double tmin, Hit& h) {
   h.u = 0.0, h.v = 0.0;
   hit_prim<UV>(S.prims + best, o, d, tmin, kInf, h);
-  h.lazy_sphere = (!UV && S.prims[best].kind == RTX_PRIM_SPHERE) ? best : -1;
+  h.lazy_uv = (!UV && S.prims[best].kind == RTX_PRIM_SPHERE) ? best : -1;
 }
 
 // The same record from the winner's distance t as traversal computed it (prim_t returns
@@ -595,7 +598,7 @@ __device__ __forceinline__ void finish_hit_at(const DScene& S, int64_t best, dou
   h.u = 0.0, h.v = 0.0;
   h.mat = P->material;
   h.t = t;
-  h.lazy_sphere = -1;
+  h.lazy_uv = -1;
   if (kind == RTX_PRIM_SPHERE) {  // hit_sphere after the root
     const V3 c{P->g[0], P->g[1], P->g[2]};
     const double radius = fmax(0.0, P->g[3]);
@@ -603,7 +606,7 @@ __device__ __forceinline__ void finish_hit_at(const DScene& S, int64_t best, dou
     const V3 outward = (h.p - c) / radius;
     set_face_normal(h, d, outward);
     if (UV) sphere_uv(outward, h.u, h.v);
-    else h.lazy_sphere = best;
+    else h.lazy_uv = best;
   } else if (kind == RTX_PRIM_TRIANGLE) {  // hit_triangle after t
     const V3 e1 = tri_e1(P->g), e2 = tri_e2(P->g);
     h.p = o + h.t * d;
@@ -614,10 +617,14 @@ __device__ __forceinline__ void finish_hit_at(const DScene& S, int64_t best, dou
     if (kind == RTX_PRIM_XY_RECT) a0 = 0, a1 = 1, n = v3(0, 0, 1);
     else if (kind == RTX_PRIM_XZ_RECT) a0 = 0, a1 = 2, n = v3(0, 1, 0);
     else a0 = 1, a1 = 2, n = v3(1, 0, 0);
-    const double x = comp(o, a0) + t * comp(d, a0);
-    const double y = comp(o, a1) + t * comp(d, a1);
-    h.u = (x - P->g[0]) / (P->g[1] - P->g[0]);
-    h.v = (y - P->g[2]) / (P->g[3] - P->g[2]);
+    if (UV || !RTX_LAZY_RECT_UV) {
+      const double x = comp(o, a0) + t * comp(d, a0);
+      const double y = comp(o, a1) + t * comp(d, a1);
+      h.u = (x - P->g[0]) / (P->g[1] - P->g[0]);
+      h.v = (y - P->g[2]) / (P->g[3] - P->g[2]);
+    } else {
+      h.lazy_uv = best;  // x, y above are p's components (lazy_uv)
+    }
     set_face_normal(h, d, n);
     h.p = o + h.t * d;
   }
@@ -1416,7 +1423,10 @@ __device__ __forceinline__ int64_t trace_fast4_lean(const DScene& S, V3 o, V3 d,
 // ---------------------------------------------------------------------------------------
 // Textures / materials
 // ---------------------------------------------------------------------------------------
-// Deferred get_sphere_uv for image textures: outward = (p - c) / r exactly as hit_sphere.
+// Deferred u,v for image textures: a sphere's get_sphere_uv with outward = (p - c) / r exactly
+// as hit_sphere; a rect's (x - x0) / (x1 - x0), (y - y0) / (y1 - y0) (rect.h), where x and y
+// are p's in-plane components (hit_rect's x = o + t d per component, the same operations as
+// p = o + t d).
 // (Returned by value: reference outputs of a call live in scratch memory.)
 #ifndef RTX_LAZY_UV_INLINE
 #define RTX_LAZY_UV_INLINE 0  // 1: inlined instead of called
@@ -1426,11 +1436,18 @@ __device__ __forceinline__
 #else
 __device__ __noinline__
 #endif
-double2 lazy_sphere_uv(const rtx_prim* __restrict__ P, V3 p) {
-  V3 c{P->g[0], P->g[1], P->g[2]};
-  double radius = fmax(0.0, P->g[3]);
+double2 lazy_uv(const rtx_prim* __restrict__ P, V3 p) {
   double2 uv;
-  sphere_uv((p - c) / radius, uv.x, uv.y);
+  const int kind = P->kind;
+  if (kind == RTX_PRIM_SPHERE) {
+    V3 c{P->g[0], P->g[1], P->g[2]};
+    double radius = fmax(0.0, P->g[3]);
+    sphere_uv((p - c) / radius, uv.x, uv.y);
+  } else {
+    const int a0 = kind == RTX_PRIM_YZ_RECT ? 1 : 0, a1 = kind == RTX_PRIM_XY_RECT ? 1 : 2;
+    uv.x = (comp(p, a0) - P->g[0]) / (P->g[1] - P->g[0]);
+    uv.y = (comp(p, a1) - P->g[2]) / (P->g[3] - P->g[2]);
+  }
   return uv;
 }
 
@@ -1451,8 +1468,8 @@ __device__ __forceinline__ V3 tex_value(const DScene& S, int32_t t, const Hit& r
     if (T.image < 0) return v3(0, 1, 1);
     const DImage im = S.images[T.image];
     if (im.h <= 0) return v3(0, 1, 1);
-    if (rec.lazy_sphere >= 0) {
-      const double2 uv = lazy_sphere_uv(S.prims + rec.lazy_sphere, p);
+    if (rec.lazy_uv >= 0) {
+      const double2 uv = lazy_uv(S.prims + rec.lazy_uv, p);
       u = uv.x, v = uv.y;
     }
     u = u < 0 ? 0 : (u > 1 ? 1 : u);

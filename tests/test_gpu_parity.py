@@ -313,3 +313,51 @@ def test_parked_traversal_schedule_is_bit_identical(rtx_mod, dev_scenes, scene, 
     assert sta["parked"] == 0 and stb["parked"] == (1 if fast4 else 0) and stc["parked"] in (0, 1)
     assert np.array_equal(a, b) and np.array_equal(sa, sb) and sta["rays_total"] == stb["rays_total"]
     assert np.array_equal(a, c) and np.array_equal(sa, sc)
+
+
+# A Cornell box with earthmap on its walls, an earthmap-textured emitter, an image-textured
+# sphere and a checker rect.  The checker's cell boundaries are kept off every rect's plane:
+# where floor(p / scale) sits at a boundary (a rect at x = 0 or 10 with scale 0.5), a last-ulp
+# difference of p (device vs glibc cos/sin in an earlier bounce) flips the cell.
+TEXTURED_RECTS = """rtxscene 1
+bvh 1
+tex 0 image earthmap
+mat 0 lambertian 0
+tex 1 solid 0.72999999999999998 0.72999999999999998 0.72999999999999998
+tex 2 solid 0.12 0.45000000000000001 0.14999999999999999
+tex 3 checker 0.37 1 2
+mat 1 lambertian 3
+tex 4 solid 15 15 15
+mat 2 light 4
+tex 5 image earthmap
+mat 3 light 5
+rect yz 0 10 0 10 10 0
+rect yz 0 10 0 10 0 0
+rect xz 0 10 0 10 0 0
+rect xz 0 10 0 10 10 0
+rect xy 0 10 0 10 10 0
+rect xz 3 7 3 7 9.9900000000000002 2
+rect xy 1 3 1 3 9.5 3
+rect xz 6 9 6 9 0.29999999999999999 1
+sphere 5 2 5 1.5 0
+"""
+
+
+@pytest.mark.parametrize("precision", ["parity", "fast"])
+def test_image_textured_rects(rtx_mod, orc, tmp_path, gpu, precision):
+    """Image textures on rects (u,v from rect.h) and on a sphere, an image-textured emitter and
+    a checker: the persistent kernel derives a rect's u,v from the hit point only at the texture
+    lookup (lazy_uv), the wavefront computes them at hit time; both must give the same pixels,
+    and match the oracle."""
+    path = str(tmp_path / "textured_rects.rtxs")
+    open(path, "w").write(TEXTURED_RECTS)
+    d = rtx_mod.DeviceScene(rtx_mod.HostScene.load(path))
+    cam = rtx_mod.camera(rtx_mod.camera_config("cornell", width=48))
+    a, sa, _ = d.render(cam, 6, 20, seed=5, adaptive=0, mode="wavefront", precision=precision)
+    b, sb, _ = d.render(cam, 6, 20, seed=5, adaptive=0, mode="persistent", precision=precision)
+    assert np.array_equal(a, b) and np.array_equal(sa, sb)
+    ref, _, _ = orc.Scene(path).render(orc.camera_preset("cornell"), 48, 6, 20, 5, adaptive=0, rng="philox",
+                                       mode="per_pixel", threads=8)
+    rms = np.sqrt(np.mean((b - ref.reshape(-1, 3)) ** 2))
+    assert rms <= RMS_TOL, rms
+    assert np.abs(b).max() > 0
