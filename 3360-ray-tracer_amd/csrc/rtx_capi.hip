@@ -1074,7 +1074,7 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
       // fixed spp: only sum/(float)samples reaches the output, and the in-order sum is the
       // same as RecordSample's; the Welford mean/M2 (three divisions per sample) only feed
       // IsConverged, which adaptive sampling alone consults
-      hipLaunchKernelGGL(k_accumulate_sum, dim3((unsigned)((npix + kAccWave - 1) / kAccWave)), dim3(kAccWave), 0, s, px,
+      hipLaunchKernelGGL(k_accumulate_sum, dim3((unsigned)((npix + kAccPix - 1) / kAccPix)), dim3(kAccWave), 0, s, px,
                          A.L, npix, Kc);
     else
       hipLaunchKernelGGL(k_accumulate, dim3(pix_blocks), dim3(kBlock), 0, s, px, A.L, npix, Kc, prm->adaptive,

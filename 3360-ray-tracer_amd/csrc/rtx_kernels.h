@@ -637,19 +637,27 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(PixelSoA px, const double
 // the runs are not 16-byte aligned, i.e. K odd, or for a short last chunk), all issued before
 // the first LDS store, then each lane adds its own pixel's samples in order.
 #ifndef RTX_ACC_CHUNK
-#define RTX_ACC_CHUNK 4  // samples per LDS-staged chunk of the fixed-spp accumulate (4 > 8 > 16, ab_acc_pipe)
+#define RTX_ACC_CHUNK 8  // samples per LDS-staged chunk of the fixed-spp accumulate (with 16 pixels per workgroup; ab_acc*)
+#endif
+#ifndef RTX_ACC_NT
+#define RTX_ACC_NT 0  // accumulate: the radiance records read with non-temporal (streaming) loads
 #endif
 #ifndef RTX_ACC_PIPE
 #define RTX_ACC_PIPE 1  // accumulate: the next chunk's loads are in flight while the current one is summed
 #endif
-constexpr int kAccWave = 64, kAccChunk = RTX_ACC_CHUNK, kAccPitch = 3 * kAccChunk + 1;  // odd pitch: spread LDS banks
+#ifndef RTX_ACC_PIX
+#define RTX_ACC_PIX 16  // accumulate: pixels per 64-lane workgroup (fewer: less LDS, more workgroups per CU; ab_acc*)
+#endif
+constexpr int kAccWave = 64, kAccPix = RTX_ACC_PIX, kAccChunk = RTX_ACC_CHUNK,
+              kAccPitch = 3 * kAccChunk + 1;  // odd pitch: spread LDS banks
+static_assert(kAccPix <= kAccWave, "one summing lane per pixel");
 #ifndef RTX_PERSISTENT_ONLY  // rtx_park.hip: the persistent kernel's PARK instantiations only
 __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const double* __restrict__ L, int64_t npix,
                                                              int K) {
-  __shared__ double st[kAccWave * kAccPitch];
+  __shared__ double st[kAccPix * kAccPitch];
   const int t = threadIdx.x;
-  const int64_t p0 = (int64_t)blockIdx.x * kAccWave;
-  const int npx = (int)std::min<int64_t>(kAccWave, npix - p0);
+  const int64_t p0 = (int64_t)blockIdx.x * kAccPix;
+  const int npx = (int)std::min<int64_t>(kAccPix, npix - p0);
   const int64_t p = p0 + t;
   const double* __restrict__ base = L + p0 * 3 * (int64_t)K;
   double sum[3] = {0, 0, 0};
@@ -659,20 +667,30 @@ __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const 
   // Full chunks with 16-byte-aligned runs (K even) are software-pipelined: chunk i + 1 is
   // loaded into registers before chunk i is summed out of LDS.  Same adds, same order.
   constexpr int PP = 3 * kAccChunk / 2;  // 16-byte pieces per pixel run
+  constexpr int NL = (kAccPix * PP + kAccWave - 1) / kAccWave;  // 16-byte loads per lane per chunk
   const int kfull = (K & 1) == 0 ? (K / kAccChunk) * kAccChunk : 0;
   if (kfull > 0) {
-    double2 v[PP];
+    double2 v[NL];
     auto load = [&](int k0) {
 #pragma unroll
-      for (int i = 0; i < PP; i++) {
+      for (int i = 0; i < NL; i++) {
         const int e = t + kAccWave * i, q = e / PP, j = e - q * PP;
-        if (q < npx) v[i] = *(const double2*)(base + (int64_t)q * 3 * K + 3 * k0 + 2 * j);
+        if (q < npx) {
+          const double2* a = (const double2*)(base + (int64_t)q * 3 * K + 3 * k0 + 2 * j);
+#if RTX_ACC_NT
+          typedef double d2v __attribute__((ext_vector_type(2)));
+          const d2v t = __builtin_nontemporal_load((const d2v*)a);
+          v[i] = make_double2(t.x, t.y);
+#else
+          v[i] = *a;
+#endif
+        }
       }
     };
     load(0);
     for (int k0 = 0; k0 < kfull; k0 += kAccChunk) {
 #pragma unroll
-      for (int i = 0; i < PP; i++) {
+      for (int i = 0; i < NL; i++) {
         const int e = t + kAccWave * i, q = e / PP, j = e - q * PP;
         if (q < npx) st[q * kAccPitch + 2 * j] = v[i].x, st[q * kAccPitch + 2 * j + 1] = v[i].y;
       }
@@ -692,14 +710,15 @@ __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const 
     const int kc = std::min(kAccChunk, K - k0);
     if (kc == kAccChunk && (K & 1) == 0) {
       constexpr int PP = 3 * kAccChunk / 2;  // 16-byte pieces per pixel run
-      double2 v[PP];
+      constexpr int NL = (kAccPix * PP + kAccWave - 1) / kAccWave;
+      double2 v[NL];
 #pragma unroll
-      for (int i = 0; i < PP; i++) {
+      for (int i = 0; i < NL; i++) {
         const int e = t + kAccWave * i, q = e / PP, j = e - q * PP;
         if (q < npx) v[i] = *(const double2*)(base + (int64_t)q * 3 * K + 3 * k0 + 2 * j);
       }
 #pragma unroll
-      for (int i = 0; i < PP; i++) {
+      for (int i = 0; i < NL; i++) {
         const int e = t + kAccWave * i, q = e / PP, j = e - q * PP;
         if (q < npx) st[q * kAccPitch + 2 * j] = v[i].x, st[q * kAccPitch + 2 * j + 1] = v[i].y;
       }
