@@ -367,9 +367,6 @@ __device__ __forceinline__ bool hit_sphere(const double* g, int32_t mat, V3 o, V
 #ifndef RTX_KIND_UNPINNED
 #define RTX_KIND_UNPINNED 1  // kind-specialised primitive tests do not load the kind word (A/B r02: bunny +0.3 %, C5 +0.3 %)
 #endif
-#ifndef RTX_SPH_BRANCHLESS
-#define RTX_SPH_BRANCHLESS 0  // traversal's sphere test: 1 no early exits, 2 only the far root conditional (A/B r02: -2.5 % / +-0 C2)
-#endif
 __device__ __forceinline__ V3 tri_e1(const double* g) {
   if (RTX_TRI_EDGES) return V3{g[3], g[4], g[5]};
   return V3{g[3], g[4], g[5]} - V3{g[0], g[1], g[2]};
@@ -542,17 +539,9 @@ __device__ __forceinline__ bool prim_t(const rtx_prim* __restrict__ Pp, bool tri
     double h = dot(d, oc);
     double cc = len2(oc) - radius * radius;
     double disc = h * h - a * cc;
-    if (RTX_SPH_BRANCHLESS == 1) {  // both roots, no early exit (sqrt of disc < 0 is NaN: both fail)
-      const double sq = sqrt(disc);
-      const double r1 = (h - sq) / a, r2 = (h + sq) / a;
-      const bool ok1 = tmin < r1 && r1 < tmax, ok2 = tmin < r2 && r2 < tmax;
-      t_out = ok1 ? r1 : r2;
-      return !(disc < 0) & (ok1 | ok2);
-    }
-    if (!RTX_SPH_BRANCHLESS && disc < 0) return false;
+    if (disc < 0) return false;  // (no gain without the early exits: ledger, ab_sph_*)
     double sq = sqrt(disc);
     double root = (h - sq) / a;
-    if (RTX_SPH_BRANCHLESS && disc < 0) return false;
     if (!(tmin < root && root < tmax)) {
       root = (h + sq) / a;
       if (!(tmin < root && root < tmax)) return false;
@@ -1065,9 +1054,6 @@ __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, doub
 #ifndef RTX_PUSH_BRANCHLESS
 #define RTX_PUSH_BRANCHLESS 1  // lean walk: unconditional child stores, sp advanced per entered child
 #endif
-#ifndef RTX_POP_BRANCHLESS
-#define RTX_POP_BRANCHLESS 0  // lean walk: stack pop without a branch (read below sp, select)
-#endif
 #ifndef RTX_PK_SLAB
 #define RTX_PK_SLAB 0  // lean walk: slab plane distances with packed f32 FMAs (A/B r02: bit-identical, -2.6 % C2, -3.9 % bunny, -5.8 % C5; off)
 #endif
@@ -1339,24 +1325,6 @@ __device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double t
     cswap4(tt[0], cc[0], tt[2], cc[2]);
     cswap4(tt[1], cc[1], tt[3], cc[3]);
     cswap4(tt[1], cc[1], tt[2], cc[2]);
-#if RTX_PUSH_BRANCHLESS && RTX_POP_BRANCHLESS
-    // push and pop without a branch: the pushes are stored and counted as below (a visit
-    // that enters no child advances sp by nothing, its stores land just above the top), then
-    // every lane reads the slot below sp and keeps it only when it entered nothing
-    {
-      const bool enter = tt[0] != __builtin_inff();
-#pragma unroll
-      for (int c = 3; c >= 1; c--) {
-        stk[sp * stride] = (uint32_t)cc[c];
-        sp += tt[c] != __builtin_inff() ? 1 : 0;
-      }
-      if (!enter && sp == 0) break;
-      const uint32_t top = stk[(sp > 0 ? sp - 1 : 0) * stride];
-      node = enter ? (uint32_t)cc[0] : top;
-      sp -= enter ? 0 : 1;
-      continue;
-    }
-#endif
     if (tt[0] != __builtin_inff()) {
 #if RTX_PUSH_BRANCHLESS
       // The sort leaves the entered children as a prefix (the others carry +inf and sort

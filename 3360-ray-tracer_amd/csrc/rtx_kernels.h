@@ -639,9 +639,6 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(PixelSoA px, const double
 #ifndef RTX_ACC_CHUNK
 #define RTX_ACC_CHUNK 8  // samples per LDS-staged chunk of the fixed-spp accumulate (with 16 pixels per workgroup; ab_acc*)
 #endif
-#ifndef RTX_ACC_NT
-#define RTX_ACC_NT 0  // accumulate: the radiance records read with non-temporal (streaming) loads
-#endif
 #ifndef RTX_ACC_PIPE
 #define RTX_ACC_PIPE 1  // accumulate: the next chunk's loads are in flight while the current one is summed
 #endif
@@ -675,16 +672,7 @@ __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const 
 #pragma unroll
       for (int i = 0; i < NL; i++) {
         const int e = t + kAccWave * i, q = e / PP, j = e - q * PP;
-        if (q < npx) {
-          const double2* a = (const double2*)(base + (int64_t)q * 3 * K + 3 * k0 + 2 * j);
-#if RTX_ACC_NT
-          typedef double d2v __attribute__((ext_vector_type(2)));
-          const d2v t = __builtin_nontemporal_load((const d2v*)a);
-          v[i] = make_double2(t.x, t.y);
-#else
-          v[i] = *a;
-#endif
-        }
+        if (q < npx) v[i] = *(const double2*)(base + (int64_t)q * 3 * K + 3 * k0 + 2 * j);
       }
     };
     load(0);
