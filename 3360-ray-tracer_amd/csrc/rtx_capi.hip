@@ -90,6 +90,8 @@ float round_up(double x) {
 
 }  // namespace
 
+constexpr int kCounterWords = 64 + 8 * 16;  // statistics, queue counts, slot counter(s)
+
 struct rtx_scene {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -968,7 +970,7 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
   if ((rc = sc->px_samples.reserve(npix * sizeof(int32_t)))) return rc;
   if ((rc = sc->px_conv.reserve(npix))) return rc;
   if ((rc = sc->lbuf.reserve(nslots * 3 * sizeof(double)))) return rc;
-  if ((rc = sc->counters.reserve(64 * sizeof(unsigned long long)))) return rc;
+  if ((rc = sc->counters.reserve(kCounterWords * sizeof(unsigned long long)))) return rc;
   const size_t qbytes = nslots * (9 * sizeof(double) + 3 * sizeof(uint32_t));
   if (prm->mode == RTX_MODE_WAVEFRONT)
     for (auto& q : sc->queue)
@@ -978,7 +980,7 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
   HIPC(hipMemsetAsync(sc->px_m2.p, 0, npix * 3 * sizeof(double), s));
   HIPC(hipMemsetAsync(sc->px_samples.p, 0, npix * sizeof(int32_t), s));
   HIPC(hipMemsetAsync(sc->px_conv.p, 0, npix, s));
-  HIPC(hipMemsetAsync(sc->counters.p, 0, 64 * sizeof(unsigned long long), s));
+  HIPC(hipMemsetAsync(sc->counters.p, 0, kCounterWords * sizeof(unsigned long long), s));
 
   unsigned long long* cnt = sc->counters.as<unsigned long long>();
   PixelSoA px{sc->px_sum.as<double>(), sc->px_mean.as<double>(), sc->px_m2.as<double>(), sc->px_samples.as<int32_t>(),
@@ -997,9 +999,10 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
   // the lean BVH4 walk stores at most fast_need + 1 stack slots (RTX_PUSH_BRANCHLESS); the
   // parity walk gets its template bound (pick_stack: reference depth + 2)
   A.stack_slots = (fast && RTX_NODE_LEAN && RTX_PUSH_BRANCHLESS) ? sc->fast_need + 1 : L.stack + 1;
-  // counters[8..] : queue counts (u32) for the wavefront, [16] slot counter (persistent)
+  // counters[8..] : queue counts (u32) for the wavefront, [16] slot counter (persistent);
+  // [64 + 16 g] the slot counters of the 8 regions (RTX_XCD_REGIONS), 128 bytes apart
   unsigned* qcount = (unsigned*)(cnt + 8);
-  unsigned long long* next_slot = cnt + 16;
+  unsigned long long* next_slot = RTX_XCD_REGIONS ? cnt + 64 : cnt + 16;
   auto make_queue = [&](DevBuf& b) {
     PathQueue q;
     double* d = b.as<double>();
@@ -1060,7 +1063,7 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
         hot_launches++;
       }
     } else {
-      HIPC(hipMemsetAsync(next_slot, 0, sizeof(unsigned long long), s));
+      HIPC(hipMemsetAsync(next_slot, 0, (RTX_XCD_REGIONS ? 8 * 16 : 1) * sizeof(unsigned long long), s));
       if ((rc = hot_begin())) return rc;
       rc = prm->mode == RTX_MODE_MEGAKERNEL ? persist_m<true>(L, A, next_slot) : persist_m<false>(L, A, next_slot);
       if (rc) return rc;

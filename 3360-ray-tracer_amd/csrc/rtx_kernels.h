@@ -331,6 +331,9 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in,
 #ifndef RTX_PARK
 #define RTX_PARK 16  // persistent (PARK kernel): park traversals once at most this many lanes still walk (A/B r01: 16 best for the bunny; 0: no PARK kernel)
 #endif
+#ifndef RTX_XCD_REGIONS
+#define RTX_XCD_REGIONS 1  // persistent: slots drawn from 8 per-XCD-group regions (image bands) instead of one counter (A/B r02: C3 +2.9 %, C2 +2.3 %, C4 +2.7 %)
+#endif
 #ifndef RTX_CHUNK
 #define RTX_CHUNK 256  // persistent: slots taken per atomic on the global slot counter
 #endif
@@ -361,6 +364,8 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
   uint32_t segs = 0, prims = 0;
   uint64_t chunk_base = 0, chunk_left = 0;  // wave-uniform
   bool exhausted = false;                   // wave-uniform
+  uint32_t region = blockIdx.x & 7;         // wave-uniform (RTX_XCD_REGIONS)
+  (void)region;
   bool has = false;
   Path P;
   P.depth = 0;
@@ -400,6 +405,30 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
       if (chunk_left >= nidle) {
         if (!has) cand = chunk_base + rank;
         chunk_base += nidle, chunk_left -= nidle;
+      } else if (RTX_XCD_REGIONS) {
+        // the slot range is cut into 8 contiguous regions (bands of the image), one counter
+        // each; a wave drains the region of its XCD group (blockIdx % 8: blocks b and b + 8
+        // share an XCD and its L2), then moves on to the next ones (load balance at the end).
+        // Which wave renders a slot changes, not what it computes.
+        uint64_t nb = ~0ull, ne = 0;
+        for (int tries = 0; tries < 8 && nb == ~0ull; tries++) {
+          unsigned long long b = 0;
+          if (lane_id() == 0) b = atomicAdd(next_slot + 16 * region, (unsigned long long)kChunk);
+          b = __shfl(b, 0);
+          const uint64_t rs = ((uint64_t)region * nslots) >> 3, re = ((uint64_t)(region + 1) * nslots) >> 3;
+          if (rs + b < re) nb = rs + b, ne = std::min<uint64_t>(rs + b + kChunk, re);
+          else region = (region + 1) & 7;
+        }
+        if (!has) {
+          if (rank < chunk_left) cand = chunk_base + rank;
+          else if (nb != ~0ull && nb + (rank - chunk_left) < ne) cand = nb + (rank - chunk_left);
+        }
+        if (nb != ~0ull) {
+          const uint64_t used = std::min<uint64_t>(nidle - chunk_left, ne - nb);
+          chunk_base = nb + used, chunk_left = (ne - nb) - used;
+        } else {
+          chunk_left = 0, exhausted = true;
+        }
       } else {
         unsigned long long nb = 0;
         if (lane_id() == 0) nb = atomicAdd(next_slot, (unsigned long long)kChunk);
