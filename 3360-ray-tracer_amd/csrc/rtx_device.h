@@ -488,9 +488,21 @@ __device__ __forceinline__ PrimRec load_prim(const rtx_prim* __restrict__ P, boo
 // KIND >= 0: every primitive this call can see has that kind (DScene::tree_kind), so the
 // other kinds' branches are compiled out.
 template <int KIND = -1>
+__device__ __forceinline__ PrimRec load_prim_k(const rtx_prim* __restrict__ Pp, bool tris) {
+  return load_prim<(KIND >= 0)>(Pp, KIND < 0 ? tris : KIND == (int)RTX_PRIM_TRIANGLE);
+}
+template <int KIND = -1>
+__device__ __forceinline__ bool prim_t_rec(const PrimRec& R, V3 o, V3 d, double tmin, double tmax, double& t_out,
+                                           int32_t& mat_out);
+template <int KIND = -1>
 __device__ __forceinline__ bool prim_t(const rtx_prim* __restrict__ Pp, bool tris, V3 o, V3 d, double tmin,
                                        double tmax, double& t_out, int32_t& mat_out) {
-  const PrimRec R = load_prim<(KIND >= 0)>(Pp, KIND < 0 ? tris : KIND == (int)RTX_PRIM_TRIANGLE);
+  return prim_t_rec<KIND>(load_prim_k<KIND>(Pp, tris), o, d, tmin, tmax, t_out, mat_out);
+}
+// the test itself, on a record already loaded
+template <int KIND>
+__device__ __forceinline__ bool prim_t_rec(const PrimRec& R, V3 o, V3 d, double tmin, double tmax, double& t_out,
+                                           int32_t& mat_out) {
   mat_out = R.mat;
   const PrimRec* P = &R;
   const int kind = KIND >= 0 ? KIND : P->kind;
@@ -1201,12 +1213,144 @@ __device__ __forceinline__ void pooled_leaf_tests(const DScene& S, V3 o, V3 d, d
   __builtin_amdgcn_wave_barrier();
 }
 
+#ifndef RTX_LEAF_STEP
+// lean walk: at most one leaf test per lane and loop iteration (trace4_run_step); the PARK TU
+// sets 1 (A/B r02: bunny +2.8 %, C2 -1.5 %, C5 -1.9 %)
+#define RTX_LEAF_STEP 0
+#endif
+// The lean walk with its leaf tests spread over loop iterations.  A node visit whose boxes
+// admit L leaf slots keeps the lane on that node for max(1, L) iterations: the slab tests and
+// the first leaf test in the first, one more leaf test in each further one, and the stack
+// update (cull by the new closest distance, sort, push / pop) in the last.  Each lane runs the
+// same node visits and primitive tests in the same order as trace4_run (same results, bit for
+// bit); what changes is how a wave's lanes line up.  trace4_run gives each node iteration a
+// leaf loop as long as the longest lane's (1-4 trips of ~5 active lanes on the bunny), while
+// here lanes with more leaves carry them into iterations where the other lanes visit nodes,
+// so a wave iteration is one node phase plus at most one leaf test.  A lane parks only
+// between node visits (no leaf pending), so the parked state is the same TravState.
+template <int STACK, bool COUNT, int KIND = -1>
+__device__ __forceinline__ bool trace4_run_step(const DScene& S, V3 o, V3 d, double tmin, uint32_t* stk,
+                                                int stride, Counters& cnt, TravState& ts, int park_at) {
+  FRay4L r = make_fray4l(o, d);
+  const char* __restrict__ nbase = (const char*)S.f4nodes;
+  double closest = ts.closest, t;
+  int32_t best = ts.best, mat_best = ts.mat, m;
+  float tmax_f = ts.tmax_f;
+  float tmax_x = tmax_f * 1.00001f;
+  int sp = ts.sp;
+  uint32_t node = ts.node;
+  bool done = true, pending = false, shrink = false;
+  uint32_t lmask = 0;
+  float tt[4];
+  int32_t cc[4];
+  while (true) {
+    // every lane still in the loop counts as walking, parking takes only lanes between visits
+    const bool park = park_at >= 0 && __popcll(__ballot(1)) <= park_at;
+#if RTX_LEAF_STEP == 2
+    // RTX_LEAF_STEP 2: a visit's leaf slots are tested from the next iteration on, each with
+    // its record load issued at the top of the iteration, beside the other lanes' node loads
+    const bool leaf = lmask != 0;
+    PrimRec R;
+    uint32_t cur = 0;
+    if (leaf) {
+      const int c = __builtin_ctz(lmask);
+      lmask &= lmask - 1u;
+      const int32_t c01 = (c & 1) ? cc[1] : cc[0], c23 = (c & 1) ? cc[3] : cc[2];
+      cur = ~(uint32_t)((c & 2) ? c23 : c01);
+      R = load_prim_k<KIND>(S.prims + cur, S.has_tris);
+    }
+#endif
+    if (!pending) {
+      if (park) {
+        done = false;
+        break;
+      }
+      const uint32_t noff = node << 7;  // sizeof(F4Node) == 128
+      if (COUNT) {
+        cnt.nodes++;
+        if (first_active_lane()) cnt.wnodes++;
+      }
+      const int4 ch = *(const int4*)(nbase + (noff + 96u));
+      const float4 ex = *(const float4*)(nbase + (noff + r.ox)), fx = *(const float4*)(nbase + (noff + (r.ox ^ 16u)));
+      const float4 ey = *(const float4*)(nbase + (noff + r.oy)), fy = *(const float4*)(nbase + (noff + (r.oy ^ 16u)));
+      const float4 ez = *(const float4*)(nbase + (noff + r.oz)), fz = *(const float4*)(nbase + (noff + (r.oz ^ 16u)));
+      cc[0] = ch.x, cc[1] = ch.y, cc[2] = ch.z, cc[3] = ch.w;
+      lmask = 0;
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const float tn = fmaxf(fmaxf(fmaf(f4c(ex, c), r.iex, r.nex), fmaf(f4c(ey, c), r.iey, r.ney)),
+                               fmaxf(fmaf(f4c(ez, c), r.iez, r.nez), 0.0f));
+        const float tf = fminf(fminf(fmaf(f4c(fx, c), r.ixx, r.nxx), fmaf(f4c(fy, c), r.ixy, r.nxy)),
+                               fminf(fmaf(f4c(fz, c), r.ixz, r.nxz), tmax_x));
+        const bool hit = tn <= tf;
+        lmask |= (hit && cc[c] < 0) ? (1u << c) : 0u;
+        tt[c] = (hit && cc[c] >= 0) ? tn : __builtin_inff();
+      }
+      shrink = false;
+      pending = true;
+    }
+#if RTX_LEAF_STEP == 2
+    if (leaf) {
+      if (COUNT) {
+        count_prim(cnt, S.prims + cur);
+        if (first_active_lane()) cnt.wprims++;
+      }
+      if (prim_t_rec<KIND>(R, o, d, tmin, closest, t, m)) closest = t, best = (int32_t)cur, mat_best = m, shrink = true;
+    }
+#else
+    if (lmask) {  // one leaf slot, in slot order
+      const int c = __builtin_ctz(lmask);
+      lmask &= lmask - 1u;
+      const int32_t c01 = (c & 1) ? cc[1] : cc[0], c23 = (c & 1) ? cc[3] : cc[2];
+      const uint32_t cur = ~(uint32_t)((c & 2) ? c23 : c01);
+      if (COUNT) {
+        count_prim(cnt, S.prims + cur);
+        if (first_active_lane()) cnt.wprims++;
+      }
+      if (prim_t<KIND>(S.prims + cur, S.has_tris, o, d, tmin, closest, t, m))
+        closest = t, best = (int32_t)cur, mat_best = m, shrink = true;
+    }
+#endif
+    if (lmask == 0) {  // the visit is complete: stack update
+      pending = false;
+      if (shrink) {
+        tmax_f = f32_round_up(closest);
+        tmax_x = tmax_f * 1.00001f;
+#pragma unroll
+        for (int c = 0; c < 4; c++)
+          if (tt[c] > tmax_f) tt[c] = __builtin_inff();
+      }
+      cswap4(tt[0], cc[0], tt[1], cc[1]);
+      cswap4(tt[2], cc[2], tt[3], cc[3]);
+      cswap4(tt[0], cc[0], tt[2], cc[2]);
+      cswap4(tt[1], cc[1], tt[3], cc[3]);
+      cswap4(tt[1], cc[1], tt[2], cc[2]);
+      if (tt[0] != __builtin_inff()) {
+        // branchless pushes, as in trace4_run
+#pragma unroll
+        for (int c = 3; c >= 1; c--) {
+          stk[sp * stride] = (uint32_t)cc[c];
+          sp += tt[c] != __builtin_inff() ? 1 : 0;
+        }
+        node = (uint32_t)cc[0];
+      } else {
+        if (sp == 0) break;
+        node = stk[(--sp) * stride];
+      }
+    }
+  }
+  ts.node = node, ts.sp = sp, ts.closest = closest, ts.best = best, ts.mat = mat_best, ts.tmax_f = tmax_f;
+  return done;
+}
+
 template <int STACK, bool COUNT, int KIND = -1>
 __device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double tmin, uint32_t* stk, int stride,
                                            Counters& cnt, TravState& ts, int park_at, uint32_t* pool = nullptr) {
 #ifndef RTX_POOL_REMAT
 #define RTX_POOL_REMAT 1
 #endif
+  if (RTX_LEAF_STEP && !(RTX_LEAF_POOL && pool))
+    return trace4_run_step<STACK, COUNT, KIND>(S, o, d, tmin, stk, stride, cnt, ts, park_at);
   FRay4L r = make_fray4l(o, d);
   const char* __restrict__ nbase = (const char*)S.f4nodes;
   double closest = ts.closest, t;
