@@ -850,8 +850,9 @@ __device__ __forceinline__ void pin(V3& v) {
 // collapsed tree (rtx_capi.hip build_fast4).
 //
 // Slab test, one FMA per plane: t = fma(plane, inv, n) with n = -(o * inv) -/+ delta.
-// With inv = RN(1/RN(d)), o_f = RN(o), n0 = RN(-o_f * inv), the computed plane distance is
-//   t_c = T (1 + e_rel) + E,  |e_rel| <= 2^-23 + 2^-24,  |E| <= |o * inv| * 2^-23 * (1 + 2^-20)
+// With inv = 1/RN(d) to within one ulp (v_rcp_f32, RTX_SLAB_RCP; or RN(1/RN(d)), the IEEE
+// division), o_f = RN(o), n0 = RN(-o_f * inv), the computed plane distance is
+//   t_c = T (1 + e_rel) + E,  |e_rel| <= 2^-22 + 2^-24,  |E| <= |o * inv| * 2^-23 * (1 + 2^-20)
 // against the exact T = (plane - o) / d.  E is absorbed by shifting n outward by
 // delta = |n0| * 2^-20 (the entry plane's offset down, the exit plane's up, by the sign of
 // inv), e_rel by the 1e-5 relative slack on the entry/exit distances.  An axis whose offset
@@ -863,8 +864,16 @@ struct FRay4 {
   uint32_t ox, oy, oz;  // byte offset of the entry-plane array per axis (exit plane: offset ^ 16)
 #endif
 };
+#ifndef RTX_SLAB_RCP
+#define RTX_SLAB_RCP 1  // slab inverses by the hardware reciprocal (1 ulp) instead of the IEEE division sequence
+#endif
+__device__ __forceinline__ float slab_inv(float d) {
+  // a zero or denormal d gives +-inf or a huge inverse either way; the caller neutralises an
+  // axis whose offset is not finite
+  return RTX_SLAB_RCP ? __builtin_amdgcn_rcpf(d) : 1.0f / d;
+}
 __device__ __forceinline__ void fray4_axis(double o, double d, float& inv, float& nl, float& nh) {
-  inv = 1.0f / (float)d;
+  inv = slab_inv((float)d);
   const float n0 = -((float)o * inv);
   if (!(fabsf(n0) < __builtin_inff())) {
     inv = 0.0f, nl = -__builtin_inff(), nh = __builtin_inff();
@@ -881,7 +890,7 @@ __device__ __forceinline__ void fray4_axis(double o, double d, float& inv, float
 // (n0 + delta), and the entry-plane array is picked by a per-ray byte offset into the node.
 __device__ __forceinline__ void fray4_axis_signed(double o, double d, int axis, float& inv, float& nl, float& nh,
                                                   uint32_t& off) {
-  inv = 1.0f / (float)d;
+  inv = slab_inv((float)d);
   const float n0 = -((float)o * inv);
   off = 32u * axis;
   if (!(fabsf(n0) < __builtin_inff())) {
