@@ -92,6 +92,18 @@ float round_up(double x) {
 
 constexpr int kCounterWords = 64 + 8 * 16;  // statistics, queue counts, slot counter(s)
 
+// Where a render's output goes once a band of it is final (fixed-spp renders): the
+// accumulate of the last sample group runs in kBands bands of the frame's pixels, and after
+// each one `copy` enqueues that band's device-to-host copy on the copy stream, so the
+// framebuffer crosses PCIe while the next band is still being summed.  Band edges are
+// multiples of `align` pixels (whole stripes of the caller's layout).
+struct BandSink {
+  int64_t align;
+  int (*copy)(void* ctx, int64_t p0, int64_t p1, hipStream_t cs);
+  void* ctx;
+};
+constexpr int kBands = 4;
+
 struct rtx_scene {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -111,8 +123,13 @@ struct rtx_scene {
   HostBuf stage_rgb, stage_spp;  // rtx_render_multi: pinned D2H staging of this device's stripes
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> evpool;
+  // banded output copies (BandSink): a copy stream and its ordering events
+  hipStream_t copy_stream = nullptr;
+  std::vector<hipEvent_t> band_ev;
   ~rtx_scene() {
     for (auto e : evpool) (void)hipEventDestroy(e);
+    for (auto e : band_ev) (void)hipEventDestroy(e);
+    if (copy_stream) (void)hipStreamDestroy(copy_stream);
     (void)hipSetDevice(device);
     for (DevBuf* b : {&nodes, &prims, &mats, &texs, &images, &fnodes, &px_sum, &px_mean, &px_m2, &px_samples,
                       &px_conv, &lbuf, &queue[0], &queue[1], &counters, &out_rgb, &out_spp, &rays, &hits, &p3_scratch,
@@ -922,8 +939,22 @@ int64_t rtx_render_pixel_count(const rtx_camera* cam, const rtx_render_params* p
   return n;
 }
 
+static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm, double* d_rgb,
+                              int32_t* d_spp, rtx_stats* stats, void* stream, const BandSink* sink);
+// Whether render_device_impl hands a render's output to a BandSink: fixed-spp renders
+// (RecordSample's in-order sum or the megakernel's DefaultSampler) with samples to trace.
+static bool sum_path_of(const rtx_render_params* prm) {
+  const bool mk_adaptive = prm->adaptive && prm->mode == RTX_MODE_MEGAKERNEL;
+  return !mk_adaptive && (prm->mode == RTX_MODE_MEGAKERNEL || !prm->adaptive) && prm->spp > 0;
+}
+
 int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm, double* d_rgb,
                       int32_t* d_spp, rtx_stats* stats, void* stream) {
+  return render_device_impl(sc, cam, prm, d_rgb, d_spp, stats, stream, nullptr);
+}
+
+static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm, double* d_rgb,
+                              int32_t* d_spp, rtx_stats* stats, void* stream, const BandSink* sink) {
   if (!sc || !cam || !prm || !d_rgb) return fail(RTX_ERR_INVALID, "NULL argument");
   if (prm->spp < 0 || prm->max_depth < 0) return fail(RTX_ERR_INVALID, "negative spp / max_depth");
   if (prm->mode < RTX_MODE_WAVEFRONT || prm->mode > RTX_MODE_MEGAKERNEL) return fail(RTX_ERR_INVALID, "bad mode");
@@ -975,12 +1006,27 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
   if (prm->mode == RTX_MODE_WAVEFRONT)
     for (auto& q : sc->queue)
       if ((rc = q.reserve(qbytes))) return rc;
-  HIPC(hipMemsetAsync(sc->px_sum.p, 0, npix * 3 * sizeof(double), s));
-  HIPC(hipMemsetAsync(sc->px_mean.p, 0, npix * 3 * sizeof(double), s));
-  HIPC(hipMemsetAsync(sc->px_m2.p, 0, npix * 3 * sizeof(double), s));
-  HIPC(hipMemsetAsync(sc->px_samples.p, 0, npix * sizeof(int32_t), s));
-  HIPC(hipMemsetAsync(sc->px_conv.p, 0, npix, s));
+  // fixed spp (RecordSample's in-order sum, or the megakernel's DefaultSampler): only the
+  // running sum and count matter, and the first group starts them (k_accumulate_sum `first`)
+  const bool sum_path = sum_path_of(prm);
+  if (!sum_path) {
+    HIPC(hipMemsetAsync(sc->px_sum.p, 0, npix * 3 * sizeof(double), s));
+    HIPC(hipMemsetAsync(sc->px_mean.p, 0, npix * 3 * sizeof(double), s));
+    HIPC(hipMemsetAsync(sc->px_m2.p, 0, npix * 3 * sizeof(double), s));
+    HIPC(hipMemsetAsync(sc->px_samples.p, 0, npix * sizeof(int32_t), s));
+    HIPC(hipMemsetAsync(sc->px_conv.p, 0, npix, s));
+  }
   HIPC(hipMemsetAsync(sc->counters.p, 0, kCounterWords * sizeof(unsigned long long), s));
+  const bool banded = sum_path && sink && npix > 0;
+  if (banded) {
+    if (!sc->copy_stream) HIPC(hipStreamCreateWithFlags(&sc->copy_stream, hipStreamNonBlocking));
+    while (sc->band_ev.size() < kBands + 1) {
+      hipEvent_t e = nullptr;
+      HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      sc->band_ev.push_back(e);
+    }
+  }
+  bool resolved = false;
 
   unsigned long long* cnt = sc->counters.as<unsigned long long>();
   PixelSoA px{sc->px_sum.as<double>(), sc->px_mean.as<double>(), sc->px_m2.as<double>(), sc->px_samples.as<int32_t>(),
@@ -1073,22 +1119,47 @@ int rtx_render_device(rtx_scene* sc, const rtx_camera* cam, const rtx_render_par
     if (mk_adaptive)
       hipLaunchKernelGGL(k_accumulate_mk_adaptive, dim3(pix_blocks), dim3(kBlock), 0, s, px, A.L, npix, Kc,
                          prm->min_spp, prm->spp, prm->rel_threshold);
-    else if (prm->mode == RTX_MODE_MEGAKERNEL || !prm->adaptive)
+    else if (sum_path) {
       // fixed spp: only sum/(float)samples reaches the output, and the in-order sum is the
       // same as RecordSample's; the Welford mean/M2 (three divisions per sample) only feed
-      // IsConverged, which adaptive sampling alone consults
-      hipLaunchKernelGGL(k_accumulate_sum, dim3((unsigned)((npix + kAccPix - 1) / kAccPix)), dim3(kAccWave), 0, s, px,
-                         A.L, npix, Kc);
-    else
+      // IsConverged, which adaptive sampling alone consults.  The last group writes the
+      // resolved output itself (k_resolve's arithmetic), in bands when a sink takes them.
+      const bool last = s0 + Kc >= budget;
+      AccOut out{nullptr, nullptr, -1, prm->spp};
+      if (last) out = AccOut{d_rgb, d_spp, prm->mode == RTX_MODE_MEGAKERNEL ? 1 : 0, prm->spp};
+      const int nb = (last && banded) ? kBands : 1;
+      const int64_t align = banded ? std::max<int64_t>(1, sink->align) : 1;
+      const int64_t units = (npix + align - 1) / align;
+      for (int b = 0; b < nb; b++) {
+        const int64_t q0 = std::min<int64_t>(npix, units * b / nb * align);
+        const int64_t q1 = std::min<int64_t>(npix, units * (b + 1) / nb * align);
+        if (q1 <= q0) continue;
+        hipLaunchKernelGGL(k_accumulate_sum, dim3((unsigned)((q1 - q0 + kAccPix - 1) / kAccPix)), dim3(kAccWave), 0,
+                           s, px, A.L, npix, Kc, q0, q1, s0 == 0 ? 1 : 0, out);
+        HIPC(hipGetLastError());
+        if (last && banded) {
+          HIPC(hipEventRecord(sc->band_ev[b], s));
+          HIPC(hipStreamWaitEvent(sc->copy_stream, sc->band_ev[b], 0));
+          if ((rc = sink->copy(sink->ctx, q0, q1, sc->copy_stream))) return rc;
+        }
+      }
+      resolved = last;
+    } else
       hipLaunchKernelGGL(k_accumulate, dim3(pix_blocks), dim3(kBlock), 0, s, px, A.L, npix, Kc, prm->adaptive,
                          prm->min_spp, prm->rel_threshold);
     HIPC(hipGetLastError());
   }
-  hipLaunchKernelGGL(k_resolve, dim3(pix_blocks), dim3(kBlock), 0, s, px, npix,
-                     prm->mode == RTX_MODE_MEGAKERNEL ? (mk_adaptive ? 2 : 1) : 0, prm->spp, d_rgb, d_spp);
-  HIPC(hipGetLastError());
+  if (!resolved) {
+    hipLaunchKernelGGL(k_resolve, dim3(pix_blocks), dim3(kBlock), 0, s, px, npix,
+                       prm->mode == RTX_MODE_MEGAKERNEL ? (mk_adaptive ? 2 : 1) : 0, prm->spp, d_rgb, d_spp);
+    HIPC(hipGetLastError());
+  }
+  if (timed) HIPC(hipEventRecord(sc->ev[1], s));
+  if (banded) {  // the caller's stream owns the output again once the band copies are done
+    HIPC(hipEventRecord(sc->band_ev[kBands], sc->copy_stream));
+    HIPC(hipStreamWaitEvent(s, sc->band_ev[kBands], 0));
+  }
   if (timed) {
-    HIPC(hipEventRecord(sc->ev[1], s));
     HIPC(hipEventSynchronize(sc->ev[1]));
     float ms = 0;
     HIPC(hipEventElapsedTime(&ms, sc->ev[0], sc->ev[1]));
@@ -1180,9 +1251,6 @@ int render_stripes_to_host(rtx_scene* sc, const rtx_camera* cam, const rtx_rende
   int rc;
   if ((rc = sc->out_rgb.reserve(std::max<int64_t>(1, npix) * 3 * sizeof(double)))) return rc;
   if ((rc = sc->out_spp.reserve(std::max<int64_t>(1, npix) * sizeof(int32_t)))) return rc;
-  if ((rc = rtx_render_device(sc, cam, &q, sc->out_rgb.as<double>(), sc->out_spp.as<int32_t>(), st, sc->stream)))
-    return rc;
-  if (npix == 0) return RTX_OK;
   const int64_t W = map.W, H = map.H, R = map.srows, N = map.scount;
   const int64_t nblk = (H + R - 1) / R;  // stripes of the image; ours: stripe, stripe + N, ...
   const size_t row_rgb = (size_t)W * 3 * sizeof(double), row_spp = (size_t)W * sizeof(int32_t);
@@ -1190,19 +1258,45 @@ int render_stripes_to_host(rtx_scene* sc, const rtx_camera* cam, const rtx_rende
   const bool pinned = hipPointerGetAttributes(&at, out_rgb) == hipSuccess && at.type == hipMemoryTypeHost;
   (void)hipGetLastError();  // pageable memory reports an error here on some runtimes
   const int64_t full = (H / R > stripe) ? (H / R - stripe + N - 1) / N : 0;  // our stripes with R rows
-  if (pinned && full > 0) {  // whole stripes in one strided DMA, the short last stripe after it
-    HIPC(hipMemcpy2DAsync(out_rgb + (size_t)stripe * R * W * 3, (size_t)N * R * row_rgb, sc->out_rgb.p,
-                          (size_t)R * row_rgb, (size_t)R * row_rgb, (size_t)full, hipMemcpyDeviceToHost, sc->stream));
-    const int64_t rest = npix / W - full * R;
-    if (rest > 0)
-      HIPC(hipMemcpyAsync(out_rgb + (size_t)((stripe + full * N) * R) * W * 3,
-                          sc->out_rgb.as<double>() + (size_t)full * R * W * 3, (size_t)rest * row_rgb,
-                          hipMemcpyDeviceToHost, sc->stream));
-  } else {
-    if ((rc = sc->stage_rgb.reserve((size_t)npix * 3 * sizeof(double)))) return rc;
-    HIPC(hipMemcpyAsync(sc->stage_rgb.p, sc->out_rgb.p, (size_t)npix * 3 * sizeof(double), hipMemcpyDeviceToHost,
-                        sc->stream));
-  }
+  const bool direct = pinned && full > 0;  // strided DMA straight into the caller's rows
+  if (!direct && (rc = sc->stage_rgb.reserve((size_t)std::max<int64_t>(1, npix) * 3 * sizeof(double)))) return rc;
+  // Packed pixels [p0, p1) of this device's rows -> host.  Band edges are whole stripes
+  // (align R * W), so a band is a run of our full stripes (one strided DMA) and, in the last
+  // band, the short stripe at the bottom of the image.
+  struct Ctx {
+    rtx_scene* sc;
+    double* out_rgb;
+    bool direct;
+    int64_t W, R, N, stripe, full;
+    size_t row_rgb;
+  } ctx{sc, out_rgb, direct, W, R, N, stripe, full, row_rgb};
+  auto copy = [](void* c, int64_t p0, int64_t p1, hipStream_t cs) -> int {
+    const Ctx& k = *(const Ctx*)c;
+    const double* src = k.sc->out_rgb.as<double>();
+    if (!k.direct) {
+      HIPC(hipMemcpyAsync((double*)k.sc->stage_rgb.p + 3 * p0, src + 3 * p0, (size_t)(p1 - p0) * 3 * sizeof(double),
+                          hipMemcpyDeviceToHost, cs));
+      return RTX_OK;
+    }
+    const int64_t r0 = p0 / k.W, r1 = (p1 + k.W - 1) / k.W;  // packed rows
+    const int64_t k0 = r0 / k.R, k1 = std::min<int64_t>(k.full, r1 / k.R);
+    if (k1 > k0)
+      HIPC(hipMemcpy2DAsync(k.out_rgb + (size_t)(k.stripe + k0 * k.N) * k.R * k.W * 3, (size_t)k.N * k.R * k.row_rgb,
+                            src + (size_t)k0 * k.R * k.W * 3, (size_t)k.R * k.row_rgb, (size_t)k.R * k.row_rgb,
+                            (size_t)(k1 - k0), hipMemcpyDeviceToHost, cs));
+    const int64_t rs = std::max<int64_t>(r0, k.full * k.R);  // rows of the short last stripe
+    if (r1 > rs)
+      HIPC(hipMemcpyAsync(k.out_rgb + (size_t)((k.stripe + k.full * k.N) * k.R + (rs - k.full * k.R)) * k.W * 3,
+                          src + (size_t)rs * k.W * 3, (size_t)(r1 - rs) * k.row_rgb, hipMemcpyDeviceToHost, cs));
+    return RTX_OK;
+  };
+  const BandSink sink{R * W, copy, &ctx};
+  if ((rc = render_device_impl(sc, cam, &q, sc->out_rgb.as<double>(), sc->out_spp.as<int32_t>(), st, sc->stream,
+                               &sink)))
+    return rc;
+  if (npix == 0) return RTX_OK;
+  // renders the accumulate does not band (adaptive sampling) copy the whole output here
+  if (!sum_path_of(&q) && (rc = copy(&ctx, 0, npix, sc->stream))) return rc;
   if (out_spp) {
     if ((rc = sc->stage_spp.reserve((size_t)npix * sizeof(int32_t)))) return rc;
     HIPC(hipMemcpyAsync(sc->stage_spp.p, sc->out_spp.p, (size_t)npix * sizeof(int32_t), hipMemcpyDeviceToHost,
@@ -1212,7 +1306,7 @@ int render_stripes_to_host(rtx_scene* sc, const rtx_camera* cam, const rtx_rende
   int64_t r = 0;  // packed row
   for (int64_t b = stripe; b < nblk; b += N) {
     const int64_t y0 = b * R, rows = std::min<int64_t>(R, H - y0);
-    if (!pinned || full == 0)
+    if (!direct)
       std::memcpy(out_rgb + (size_t)y0 * W * 3, (const char*)sc->stage_rgb.p + (size_t)r * row_rgb,
                   (size_t)rows * row_rgb);
     if (out_spp)

@@ -1255,20 +1255,6 @@ __device__ __forceinline__ bool trace4_run_step(const DScene& S, V3 o, V3 d, dou
   while (true) {
     // every lane still in the loop counts as walking, parking takes only lanes between visits
     const bool park = park_at >= 0 && __popcll(__ballot(1)) <= park_at;
-#if RTX_LEAF_STEP == 2
-    // RTX_LEAF_STEP 2: a visit's leaf slots are tested from the next iteration on, each with
-    // its record load issued at the top of the iteration, beside the other lanes' node loads
-    const bool leaf = lmask != 0;
-    PrimRec R;
-    uint32_t cur = 0;
-    if (leaf) {
-      const int c = __builtin_ctz(lmask);
-      lmask &= lmask - 1u;
-      const int32_t c01 = (c & 1) ? cc[1] : cc[0], c23 = (c & 1) ? cc[3] : cc[2];
-      cur = ~(uint32_t)((c & 2) ? c23 : c01);
-      R = load_prim_k<KIND>(S.prims + cur, S.has_tris);
-    }
-#endif
     if (!pending) {
       if (park) {
         done = false;
@@ -1298,15 +1284,6 @@ __device__ __forceinline__ bool trace4_run_step(const DScene& S, V3 o, V3 d, dou
       shrink = false;
       pending = true;
     }
-#if RTX_LEAF_STEP == 2
-    if (leaf) {
-      if (COUNT) {
-        count_prim(cnt, S.prims + cur);
-        if (first_active_lane()) cnt.wprims++;
-      }
-      if (prim_t_rec<KIND>(R, o, d, tmin, closest, t, m)) closest = t, best = (int32_t)cur, mat_best = m, shrink = true;
-    }
-#else
     if (lmask) {  // one leaf slot, in slot order
       const int c = __builtin_ctz(lmask);
       lmask &= lmask - 1u;
@@ -1319,7 +1296,6 @@ __device__ __forceinline__ bool trace4_run_step(const DScene& S, V3 o, V3 d, dou
       if (prim_t<KIND>(S.prims + cur, S.has_tris, o, d, tmin, closest, t, m))
         closest = t, best = (int32_t)cur, mat_best = m, shrink = true;
     }
-#endif
     if (lmask == 0) {  // the visit is complete: stack update
       pending = false;
       if (shrink) {

@@ -678,16 +678,28 @@ constexpr int kAccWave = 64, kAccPix = RTX_ACC_PIX, kAccChunk = RTX_ACC_CHUNK,
               kAccPitch = 3 * kAccChunk + 1;  // odd pitch: spread LDS banks
 static_assert(kAccPix <= kAccWave, "one summing lane per pixel");
 #ifndef RTX_PERSISTENT_ONLY  // rtx_park.hip: the persistent kernel's PARK instantiations only
+// Pixels [p_begin, p_end) of the npix (one band of the frame, so the caller can copy a
+// finished band to the host while the next is summed).  first: the group starts the pixels'
+// sums (nothing to read).  resolve >= 0 (the last group): the pixel's output is written here,
+// as k_resolve would (0: sum / (float)samples, 1: the megakernel's DefaultSampler sum / spp),
+// instead of the running sum and count.
+struct AccOut {
+  double* rgb;
+  int32_t* spp_out;
+  int resolve;  // -1: keep the running sums in px; 0 / 1: write the resolved pixel
+  int spp;
+};
 __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const double* __restrict__ L, int64_t npix,
-                                                             int K) {
+                                                             int K, int64_t p_begin, int64_t p_end, int first,
+                                                             AccOut out) {
   __shared__ double st[kAccPix * kAccPitch];
   const int t = threadIdx.x;
-  const int64_t p0 = (int64_t)blockIdx.x * kAccPix;
-  const int npx = (int)std::min<int64_t>(kAccPix, npix - p0);
+  const int64_t p0 = p_begin + (int64_t)blockIdx.x * kAccPix;
+  const int npx = (int)std::min<int64_t>(kAccPix, p_end - p0);
   const int64_t p = p0 + t;
   const double* __restrict__ base = L + p0 * 3 * (int64_t)K;
   double sum[3] = {0, 0, 0};
-  if (t < npx)
+  if (t < npx && !first)
     for (int c = 0; c < 3; c++) sum[c] = px.sum[c * npix + p];
 #if RTX_ACC_PIPE
   // Full chunks with 16-byte-aligned runs (K even) are software-pipelined: chunk i + 1 is
@@ -753,8 +765,15 @@ __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const 
     __syncthreads();
   }
   if (t < npx) {
-    for (int c = 0; c < 3; c++) px.sum[c * npix + p] = sum[c];
-    px.samples[p] += K;
+    const int n = (first ? 0 : px.samples[p]) + K;
+    if (out.resolve < 0) {
+      for (int c = 0; c < 3; c++) px.sum[c * npix + p] = sum[c];
+      px.samples[p] = n;
+    } else {  // k_resolve's arithmetic (n > 0 here)
+      const double sc = out.resolve == 1 ? 1.0 / (double)out.spp : 1.0 / (double)(float)n;
+      for (int c = 0; c < 3; c++) out.rgb[3 * p + c] = sc * sum[c];
+      if (out.spp_out) out.spp_out[p] = out.resolve == 1 ? out.spp : n;
+    }
   }
 }
 #endif

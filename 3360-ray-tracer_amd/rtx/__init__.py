@@ -346,7 +346,7 @@ class DeviceScene:
 
 def render_multi(scenes, cam, spp, max_depth, seed=1234, adaptive=True, mode="persistent", precision="fast",
                  stripe_rows=8, stripe_index=0, stripe_count=0, out=None, schedule=None, min_spp=16,
-                 rel_threshold=float(np.float32(0.05))):
+                 rel_threshold=float(np.float32(0.05)), samples_per_group=0):
     """One frame over several DeviceScenes (rtx_render_multi): returns the whole-frame
     (H*W, 3) framebuffer, (H*W,) sample counts, aggregate stats, per-scene stats."""
     p = RenderParams()
@@ -355,6 +355,7 @@ def render_multi(scenes, cam, spp, max_depth, seed=1234, adaptive=True, mode="pe
     p.mode, p.precision = MODES[mode], PRECISIONS[precision]
     p.flags = SCHEDULE_FLAGS[schedule]
     p.stripe_rows, p.stripe_index, p.stripe_count = stripe_rows, stripe_index, stripe_count
+    p.samples_per_group = samples_per_group
     n = len(scenes)
     npix = cam.image_width * cam.image_height
     rgb = out if out is not None else np.zeros((npix, 3))

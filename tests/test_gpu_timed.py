@@ -227,6 +227,29 @@ def test_render_multi_into_pinned_buffer(rtx_mod, scenes):
     assert np.array_equal(out, full)
 
 
+def test_render_multi_banded_output_one_device(rtx_mod, scenes):
+    """The benchmark's path: one device, a pinned whole-frame buffer, the last sample group's
+    accumulate in bands whose device-to-host copies overlap the next band (BandSink), the
+    output resolved by the accumulate itself.  Against rtx_render (one copy at the end), for
+    one and several sample groups, a frame height that is no multiple of the stripe height,
+    and the three modes' fixed-spp sums."""
+    import torch
+
+    path, d = scenes("final")
+    cam = rtx_mod.camera(rtx_mod.camera_config("c2_final", width=76))  # 42 rows
+    npix = cam.image_width * cam.image_height
+    for mode, precision in (("persistent", "fast"), ("wavefront", "parity"), ("megakernel", "fast")):
+        for group in (0, 2):
+            full, fsp, fst = d.render(cam, 5, 50, seed=21, adaptive=False, mode=mode, precision=precision,
+                                      samples_per_group=group)
+            pinned = torch.full((npix, 3), -1.0, dtype=torch.float64).pin_memory()
+            out = pinned.numpy()
+            rgb, sp, st, _ = rtx_mod.render_multi([d], cam, 5, 50, seed=21, adaptive=False, mode=mode,
+                                                  precision=precision, out=out, samples_per_group=group)
+            assert np.array_equal(out, full) and np.array_equal(sp, fsp), (mode, group)
+            assert st["rays_total"] == fst["rays_total"]
+
+
 def test_render_multi_rejects_bad_arguments(rtx_mod, scenes):
     _, d = scenes("final")
     cam = rtx_mod.camera(rtx_mod.camera_config("c2_final", width=16))
