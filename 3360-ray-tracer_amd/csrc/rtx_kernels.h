@@ -31,7 +31,7 @@ constexpr int kBlock = 256;
 #define RTX_BVH4 1  // fast precision traverses the 4-wide collapse of the SAH tree (else BVH2)
 #endif
 #ifndef RTX_SLOT_TARGET_LOG2
-#define RTX_SLOT_TARGET_LOG2 27  // persistent: up to 2^this slots (pixel x sample) per launch (A/B r01: 27 vs 25 = +4% C2, +10% bunny)
+#define RTX_SLOT_TARGET_LOG2 29  // persistent: up to 2^this slots (pixel x sample) per launch, Lbuf <= 12.9 GB (A/B r01: 27 vs 25 = +4% C2, +10% bunny; r02: 29 vs 27 = +4.0% C4, +1.3% C5)
 #endif
 #ifndef RTX_STAMPS
 #define RTX_STAMPS 0  // diagnostic build: s_memtime per region of k_persistent -> counters[24..27]
