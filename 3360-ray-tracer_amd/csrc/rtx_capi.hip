@@ -108,7 +108,7 @@ struct rtx_scene {
   int device = 0;
   hipStream_t stream = nullptr;
   int cus = 0;
-  DevBuf nodes, prims, mats, texs, images, fnodes;
+  DevBuf nodes, prims, mats, texs, images, fnodes, tri_n;
   std::vector<DevBuf> texels;
   DScene S{};
   int stack_parity = 32, stack_fast = 32;
@@ -131,7 +131,7 @@ struct rtx_scene {
     for (auto e : band_ev) (void)hipEventDestroy(e);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
     (void)hipSetDevice(device);
-    for (DevBuf* b : {&nodes, &prims, &mats, &texs, &images, &fnodes, &px_sum, &px_mean, &px_m2, &px_samples,
+    for (DevBuf* b : {&nodes, &prims, &mats, &texs, &images, &fnodes, &tri_n, &px_sum, &px_mean, &px_m2, &px_samples,
                       &px_conv, &lbuf, &queue[0], &queue[1], &counters, &out_rgb, &out_spp, &rays, &hits, &p3_scratch,
                       &p3_body, &calib_rgb})
       b->release();
@@ -722,6 +722,29 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   for (auto& e : sc->ev) HIPC(hipEventCreate(&e));
   hipStream_t s = sc->stream;
   int rc;
+  // Triangle normals for the hit records (Triangle::Hit, triangle.h:80-82: Normalize(Cross(
+  // edge1, edge2))), formed here in the device's double operations and order (cross, len2,
+  // sqrt, 1 / l, products; no contraction), so the table holds the very bits finish_hit_at
+  // would compute per hit.
+  bool any_tri = false;
+  for (int64_t i = 0; i < d->n_prims && !any_tri; i++) any_tri = d->prims[i].kind == RTX_PRIM_TRIANGLE;
+  if (RTX_TRI_NORMALS && any_tri) {
+    std::vector<double> tn((size_t)d->n_prims * 4, 0.0);
+    for (int64_t i = 0; i < d->n_prims; i++) {
+      const rtx_prim& q = d->prims[i];
+      if (q.kind != RTX_PRIM_TRIANGLE) continue;
+      double e1[3], e2[3];
+      for (int a = 0; a < 3; a++) e1[a] = q.g[3 + a] - q.g[a], e2[a] = q.g[6 + a] - q.g[a];
+      const double c[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
+                           e1[0] * e2[1] - e1[1] * e2[0]};
+      const double l = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+      if (l == 0.0) continue;  // normalize() returns (0, 0, 0)
+      const double inv = 1.0 / l;
+      for (int a = 0; a < 3; a++) tn[4 * (size_t)i + a] = inv * c[a];
+    }
+    if ((rc = upload(sc->tri_n, tn.data(), tn.size(), s))) return rc;
+    HIPC(hipStreamSynchronize(s));  // tn is a temporary
+  }
   if (RTX_TRI_EDGES) {  // device table: triangles carry A, B - A, C - A (tri_e1 / tri_e2)
     std::vector<rtx_prim> dp(d->prims, d->prims + d->n_prims);
     for (rtx_prim& q : dp)
@@ -806,6 +829,7 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   DScene& S = sc->S;
   S.nodes = sc->nodes.as<rtx_bvh_node>();
   S.prims = sc->prims.as<rtx_prim>();
+  S.tri_n = sc->tri_n.p ? sc->tri_n.as<double>() : nullptr;
   S.mats = sc->mats.as<rtx_material>();
   S.texs = sc->texs.as<rtx_texture>();
   S.images = sc->images.as<DImage>();

@@ -297,6 +297,7 @@ struct DScene {
   int32_t no_textures;     // no material reads the texture table (solid colours resolved at upload)
   int32_t n_global;   // fast BVH: primitives kept out of the tree, tested before every walk
   int32_t global[2];  // their indices into prims (see build_global_prims, rtx_capi.hip)
+  const double* tri_n;  // RTX_TRI_NORMALS: per primitive (x, y, z, 0), a triangle's unit normal, or nullptr
 };
 
 struct Hit {  // HitRecord (hittable.h:18-42)
@@ -354,6 +355,9 @@ __device__ __forceinline__ bool hit_sphere(const double* g, int32_t mat, V3 o, V
 // same IEEE double differences on the host), so the tests read them instead of subtracting.
 #ifndef RTX_TRI_EDGES
 #define RTX_TRI_EDGES 1
+#endif
+#ifndef RTX_TRI_NORMALS
+#define RTX_TRI_NORMALS 1  // a hit triangle's unit normal read from a table formed at upload (DScene::tri_n)
 #endif
 #ifndef RTX_TRI_BRANCHLESS
 #define RTX_TRI_BRANCHLESS 0  // traversal's triangle test without early exits (prim_t): 1 in kind-specialised tests, 2 in all; the PARK TU sets 1 (A/B r02: bunny +3.8 %, C5 plain kernel -1.9 %)
@@ -609,9 +613,15 @@ __device__ __forceinline__ void finish_hit_at(const DScene& S, int64_t best, dou
     if (UV) sphere_uv(outward, h.u, h.v);
     else h.lazy_uv = best;
   } else if (kind == RTX_PRIM_TRIANGLE) {  // hit_triangle after t
-    const V3 e1 = tri_e1(P->g), e2 = tri_e2(P->g);
     h.p = o + h.t * d;
-    set_face_normal(h, d, normalize(cross(e1, e2)));
+    if (RTX_TRI_NORMALS && S.tri_n) {
+      // normalize(cross(B - A, C - A)) formed at upload in the same IEEE double operations
+      const double2 n01 = *(const double2*)(S.tri_n + 4 * best), n2 = *(const double2*)(S.tri_n + 4 * best + 2);
+      set_face_normal(h, d, V3{n01.x, n01.y, n2.x});
+    } else {
+      const V3 e1 = tri_e1(P->g), e2 = tri_e2(P->g);
+      set_face_normal(h, d, normalize(cross(e1, e2)));
+    }
   } else {  // hit_rect after t
     int a0, a1;
     V3 n;
