@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -584,6 +585,9 @@ int run_persistent_k0(const Launch& L, const RenderArgs& A, unsigned long long* 
             (TK == (int)RTX_PRIM_TRIANGLE ? RTX_BUILD_TRIANGLE_TREE : 0u) | (LAMB ? RTX_BUILD_LAMBERTIAN : 0u) |
             (NOTEX ? RTX_BUILD_NO_TEXTURES : 0u) | (NODOF ? RTX_BUILD_NO_DEFOCUS : 0u) |
             (FAST ? RTX_BUILD_FAST : 0u) | (COUNT ? RTX_BUILD_COUNT : 0u) | (SCATTER ? RTX_BUILD_SCATTER : 0u);
+  if (std::getenv("RTX_DEBUG_LAUNCH"))
+    fprintf(stderr, "rtx launch: k_persistent build 0x%x grid %d (%d blocks per CU) lds %zu B stack_slots %d\n",
+            L.build, grid, grid / std::max(1, L.sc->cus), lds, A.stack_slots);
   hipLaunchKernelGGL((k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF>), dim3(grid),
                      dim3(kBlock), lds, L.s, A, next_slot);
   HIPC(hipGetLastError());
