@@ -581,9 +581,9 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
   flush_counters(A, c, segs, prims, COUNT);
 }
 
-// The PARK instantiations are compiled in their own translation unit (rtx_park.hip) with the
-// LLVM max-memory-clause scheduler, which suits their latency-bound walk (bunny +1.5 %,
-// `ab_sched2_*`) but not the plain kernel.  Scheduling only: the same arithmetic.
+// The PARK instantiations are compiled in their own translation unit (rtx_park.hip), with
+// their own macro defaults (the leaf-step walk, the branchless triangle test) and scheduler
+// options (Makefile PARKFLAGS; the LLVM default since the leaf-step walk, `ab_sch_c3.txt`).
 #ifndef RTX_PARK_TU
 #define RTX_PARK_TU 1
 #endif

@@ -1,6 +1,6 @@
 // PARK instantiations of the persistent kernel (k_persistent<STACK, true, COUNT, SCATTER,
-// true>), compiled apart from rtx_capi.hip so this translation unit can use the LLVM
-// max-memory-clause scheduler (see the Makefile and rtx_kernels.h).
+// true>), compiled apart from rtx_capi.hip so this translation unit can have its own macro
+// defaults (below) and scheduler options (see the Makefile and rtx_kernels.h).
 #define RTX_PERSISTENT_ONLY 1
 // the library cos()/sin() here: with the small-argument form the bunny's triangle-tree
 // Lambertian build spills (0 -> 56 B per lane), see rtx_device.h

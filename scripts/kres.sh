@@ -3,7 +3,7 @@
 # (device-only compile, no GPU):  scripts/kres.sh [capi|park] [-DNAME=V ...]
 R=/root/repo/3360-ray-tracer_amd
 TU=${1:-capi}; shift
-if [ "$TU" = park ]; then F="-mllvm -amdgpu-sched-strategy=max-memory-clause"; SRC=csrc/rtx_park.hip
+if [ "$TU" = park ]; then F=""; SRC=csrc/rtx_park.hip
 else F="-mllvm -amdgpu-disable-clustered-low-occupancy-reschedule"; SRC=csrc/rtx_capi.hip; fi
 OUT=$(mktemp /tmp/kres.XXXXXX.s)
 cd $R && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -I/root/repo/include \
