@@ -860,7 +860,6 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
     S.tree_kind = k < 0 ? -1 : k;
   }
   S.global[0] = global[0], S.global[1] = global[1];
-  S.pool_ok = d->n_prims < (1ll << 26) ? 1 : 0;
   for (int64_t i = 0; i < d->n_prims && !S.has_tris; i++) S.has_tris = d->prims[i].kind == RTX_PRIM_TRIANGLE;
   if (S.use_bvh && d->nodes[0].is_leaf) S.froot_leaf = 1, S.froot_count = (int32_t)d->nodes[0].right_count;
   if (!d->nodes && d->n_nodes == 0) S.use_bvh = 0;

@@ -291,7 +291,6 @@ struct DScene {
   int32_t froot_leaf;  // fast BVH: the whole tree is one leaf (count in froot_count)
   int32_t froot_count;
   int32_t has_tris;  // any triangle: prim_t preloads all 80 record bytes, else the first 48
-  int32_t pool_ok;   // primitive indices fit the pooled leaf tests' 26-bit field
   int32_t tree_kind;  // fast BVH: the one kind of every primitive in the tree, or -1
   int32_t all_lambertian;  // every material is a Lambertian
   int32_t no_textures;     // no material reads the texture table (solid colours resolved at upload)
@@ -1085,19 +1084,6 @@ __device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, doub
 #ifndef RTX_PUSH_BRANCHLESS
 #define RTX_PUSH_BRANCHLESS 1  // lean walk: unconditional child stores, sp advanced per entered child
 #endif
-#ifndef RTX_PK_SLAB
-#define RTX_PK_SLAB 0  // lean walk: slab plane distances with packed f32 FMAs (A/B r02: bit-identical, -2.6 % C2, -3.9 % bunny, -5.8 % C5; off)
-#endif
-typedef float pk2 __attribute__((ext_vector_type(2)));
-// x * c.lo + c.hi for both halves of x in one v_pk_fma_f32: the (multiplier, addend) pair c
-// is broadcast by op_sel, so a ray's per-axis constants occupy one register pair instead of
-// two duplicated ones (the compiler materialises broadcasts as register copies).  Same
-// single-rounding fma as fmaf() per half.  ALU only.
-__device__ __forceinline__ pk2 pk_fma_bcast(pk2 x, pk2 c) {
-  pk2 r;
-  asm("v_pk_fma_f32 %0, %1, %2, %2 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(x), "v"(c));
-  return r;
-}
 struct FRay4L {
   float iex, iey, iez, nex, ney, nez;  // entry planes: inverse and offset, scaled by (1 - s)
   float ixx, ixy, ixz, nxx, nxy, nxz;  // exit planes: scaled by (1 + s)
@@ -1159,77 +1145,79 @@ __device__ __forceinline__ void trav_globals(const DScene& S, V3 o, V3 d, double
   if (S.n_global) ts.tmax_f = f32_round_up(ts.closest);
 }
 
-#ifndef RTX_LEAF_POOL
-#define RTX_LEAF_POOL 0  // lean walk: a node's leaf tests pooled across the wave (A/B r02: -45 % bunny, spills; off)
-#endif
-// Pooled leaf tests.  At a node iteration where some lane of the wave has two or more leaf
-// slots to test, the lanes' candidates (owner lane, primitive) are laid out in LDS in
-// (owner, slot) order and every lane of the wave tests one of them, with the owner's ray and
-// closest distance fetched by cross-lane reads: the wave runs ceil(T / 64) tests of all its
-// T candidates instead of (the most any lane has) tests of a few lanes each.  The owner then
-// applies its candidates' results in slot order with its running closest distance, which is
-// exactly the sequential loop: a primitive's hit test depends on the closest distance only
-// through the final t-range comparison (inclusive for triangles, strict for spheres / rects,
-// and a sphere's second root is only taken when the first lies outside the range, where it
-// stays).  `pool` = this wave's 256 LDS words (nullptr: sequential leaf loop).
-constexpr int kPoolWords = 256;  // 64 lanes x 4 leaf slots
-template <int KIND>
-__device__ __forceinline__ void pooled_leaf_tests(const DScene& S, V3 o, V3 d, double tmin, uint32_t lmask,
-                                                  const int32_t (&cc)[4], uint32_t* pool, Counters& cnt,
-                                                  bool count, double& closest, int32_t& best, int32_t& mat_best,
-                                                  bool& shrink) {
-  const int lane = (int)__lane_id();
-  const int nl = __popc(lmask);
-  const uint64_t lt = (1ull << lane) - 1ull;
-  const uint64_t b0 = __ballot(nl & 1), b1 = __ballot(nl & 2), b2 = __ballot(nl & 4);
-  const int pre = __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
-  const int T = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
-  auto cand = [&](uint32_t rest) {  // the primitive of the lowest leaf slot left in `rest`
-    const int c = __builtin_ctz(rest);
-    const int32_t c01 = (c & 1) ? cc[1] : cc[0], c23 = (c & 1) ? cc[3] : cc[2];
-    return ~(uint32_t)((c & 2) ? c23 : c01);
-  };
-  {
-    uint32_t rest = lmask;
-    for (int pos = pre; rest; rest &= rest - 1u) pool[pos++] = cand(rest) | ((uint32_t)lane << 26);
+// Pieces of a lean BVH4 node visit shared by trace4_run and trace4_run_step.
+// The slab tests of node `node`'s four slots: entry distances of the internal children entered
+// (+inf otherwise) in tt, the child words in cc; returns the mask of leaf slots entered.
+__device__ __forceinline__ uint32_t visit_slabs(const char* __restrict__ nbase, uint32_t node, const FRay4L& r,
+                                                float tmax_x, float (&tt)[4], int32_t (&cc)[4]) {
+  const uint32_t noff = node << 7;  // sizeof(F4Node) == 128
+  const int4 ch = *(const int4*)(nbase + (noff + 96u));
+  const float4 ex = *(const float4*)(nbase + (noff + r.ox)), fx = *(const float4*)(nbase + (noff + (r.ox ^ 16u)));
+  const float4 ey = *(const float4*)(nbase + (noff + r.oy)), fy = *(const float4*)(nbase + (noff + (r.oy ^ 16u)));
+  const float4 ez = *(const float4*)(nbase + (noff + r.oz)), fz = *(const float4*)(nbase + (noff + (r.oz ^ 16u)));
+  cc[0] = ch.x, cc[1] = ch.y, cc[2] = ch.z, cc[3] = ch.w;
+  uint32_t lmask = 0;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const float tn = fmaxf(fmaxf(fmaf(f4c(ex, c), r.iex, r.nex), fmaf(f4c(ey, c), r.iey, r.ney)),
+                           fmaxf(fmaf(f4c(ez, c), r.iez, r.nez), 0.0f));
+    const float tf = fminf(fminf(fmaf(f4c(fx, c), r.ixx, r.nxx), fmaf(f4c(fy, c), r.ixy, r.nxy)),
+                           fminf(fmaf(f4c(fz, c), r.ixz, r.nxz), tmax_x));
+    const bool hit = tn <= tf;
+    lmask |= (hit && cc[c] < 0) ? (1u << c) : 0u;
+    tt[c] = (hit && cc[c] >= 0) ? tn : __builtin_inff();
   }
-  __builtin_amdgcn_wave_barrier();
-  for (int base = 0; base < T; base += 64) {
-    const int j = base + lane;
-    const bool have = j < T;
-    const uint32_t e = have ? pool[j] : 0u;
-    const int owner = (int)(e >> 26);
-    const V3 oo{__shfl(o.x, owner), __shfl(o.y, owner), __shfl(o.z, owner)};
-    const V3 dd{__shfl(d.x, owner), __shfl(d.y, owner), __shfl(d.z, owner)};
-    const double cl = __shfl(closest, owner);
-    double tq = 0.0;
-    int32_t mq = -1;
-    bool hq = false, incl = false;
-    if (have) {
-      const rtx_prim* P = S.prims + (e & 0x3FFFFFFu);
-      if (count) count_prim(cnt, P);
-      hq = prim_t<KIND>(P, S.has_tris, oo, dd, tmin, cl, tq, mq);
-      incl = (KIND >= 0 ? KIND : P->kind) == (int)RTX_PRIM_TRIANGLE;
+  return lmask;
+}
+// The primitive of leaf slot c (its child word holds ~index)
+__device__ __forceinline__ uint32_t leaf_prim(const int32_t (&cc)[4], int c) {
+  const int32_t c01 = (c & 1) ? cc[1] : cc[0], c23 = (c & 1) ? cc[3] : cc[2];
+  return ~(uint32_t)((c & 2) ? c23 : c01);
+}
+// The end of a visit: after a new closest hit (shrink), the children entered beyond it are
+// dropped; the rest are sorted near to far, the nearest is visited next and the others pushed
+// (branchless, RTX_PUSH_BRANCHLESS: the sort leaves the entered children as a prefix, so the
+// stores at sp are unconditional and sp advances per entered child; build_fast4 bounds sp by
+// the tree's exact worst case, and the kernels give each lane STACK + 1 slots), or the stack
+// is popped.  false: the stack was empty, the walk is over.
+template <int STACK>
+__device__ __forceinline__ bool visit_next(float (&tt)[4], int32_t (&cc)[4], bool shrink, double closest,
+                                           float& tmax_f, float& tmax_x, uint32_t* stk, int stride, int& sp,
+                                           uint32_t& node) {
+  if (shrink) {
+    tmax_f = f32_round_up(closest);
+    tmax_x = tmax_f * 1.00001f;
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+      if (tt[c] > tmax_f) tt[c] = __builtin_inff();
+  }
+  cswap4(tt[0], cc[0], tt[1], cc[1]);
+  cswap4(tt[2], cc[2], tt[3], cc[3]);
+  cswap4(tt[0], cc[0], tt[2], cc[2]);
+  cswap4(tt[1], cc[1], tt[3], cc[3]);
+  cswap4(tt[1], cc[1], tt[2], cc[2]);
+  if (tt[0] != __builtin_inff()) {
+#if RTX_PUSH_BRANCHLESS
+#pragma unroll
+    for (int c = 3; c >= 1; c--) {
+      stk[sp * stride] = (uint32_t)cc[c];
+      sp += tt[c] != __builtin_inff() ? 1 : 0;
     }
-    if (count && first_active_lane()) cnt.wprims++;
-    const uint64_t hm = __ballot(hq), im = __ballot(hq && incl);
-    uint32_t rest = lmask;  // this lane's candidates, in slot order
-    for (int k = 0; k < 4; k++) {
-      const int p = pre + k;
-      const bool in_round = k < nl && p >= base && p < base + 64;
-      if (__ballot(in_round)) {  // positions rise with k: a later k of some lane may still fall in this round
-        const int q = in_round ? p - base : lane;
-        const double tk = __shfl(tq, q);
-        const int32_t mk = __shfl(mq, q);
-        if (in_round && ((hm >> q) & 1ull)) {
-          if (((im >> q) & 1ull) ? tk <= closest : tk < closest)
-            closest = tk, best = (int32_t)cand(rest), mat_best = mk, shrink = true;
-        }
+#else
+#pragma unroll
+    for (int c = 3; c >= 1; c--) {
+      if (tt[c] != __builtin_inff()) {
+        if (sp + 1 > STACK) __builtin_trap();
+        stk[(sp++) * stride] = (uint32_t)cc[c];
       }
-      if (k < nl) rest &= rest - 1u;
     }
+#endif
+    node = (uint32_t)cc[0];
+    return true;
   }
-  __builtin_amdgcn_wave_barrier();
+  if (sp == 0) return false;
+  node = stk[(--sp) * stride];
+  return true;
 }
 
 #ifndef RTX_LEAF_STEP
@@ -1270,35 +1258,17 @@ __device__ __forceinline__ bool trace4_run_step(const DScene& S, V3 o, V3 d, dou
         done = false;
         break;
       }
-      const uint32_t noff = node << 7;  // sizeof(F4Node) == 128
       if (COUNT) {
         cnt.nodes++;
         if (first_active_lane()) cnt.wnodes++;
       }
-      const int4 ch = *(const int4*)(nbase + (noff + 96u));
-      const float4 ex = *(const float4*)(nbase + (noff + r.ox)), fx = *(const float4*)(nbase + (noff + (r.ox ^ 16u)));
-      const float4 ey = *(const float4*)(nbase + (noff + r.oy)), fy = *(const float4*)(nbase + (noff + (r.oy ^ 16u)));
-      const float4 ez = *(const float4*)(nbase + (noff + r.oz)), fz = *(const float4*)(nbase + (noff + (r.oz ^ 16u)));
-      cc[0] = ch.x, cc[1] = ch.y, cc[2] = ch.z, cc[3] = ch.w;
-      lmask = 0;
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        const float tn = fmaxf(fmaxf(fmaf(f4c(ex, c), r.iex, r.nex), fmaf(f4c(ey, c), r.iey, r.ney)),
-                               fmaxf(fmaf(f4c(ez, c), r.iez, r.nez), 0.0f));
-        const float tf = fminf(fminf(fmaf(f4c(fx, c), r.ixx, r.nxx), fmaf(f4c(fy, c), r.ixy, r.nxy)),
-                               fminf(fmaf(f4c(fz, c), r.ixz, r.nxz), tmax_x));
-        const bool hit = tn <= tf;
-        lmask |= (hit && cc[c] < 0) ? (1u << c) : 0u;
-        tt[c] = (hit && cc[c] >= 0) ? tn : __builtin_inff();
-      }
+      lmask = visit_slabs(nbase, node, r, tmax_x, tt, cc);
       shrink = false;
       pending = true;
     }
     if (lmask) {  // one leaf slot, in slot order
-      const int c = __builtin_ctz(lmask);
+      const uint32_t cur = leaf_prim(cc, __builtin_ctz(lmask));
       lmask &= lmask - 1u;
-      const int32_t c01 = (c & 1) ? cc[1] : cc[0], c23 = (c & 1) ? cc[3] : cc[2];
-      const uint32_t cur = ~(uint32_t)((c & 2) ? c23 : c01);
       if (COUNT) {
         count_prim(cnt, S.prims + cur);
         if (first_active_lane()) cnt.wprims++;
@@ -1308,30 +1278,7 @@ __device__ __forceinline__ bool trace4_run_step(const DScene& S, V3 o, V3 d, dou
     }
     if (lmask == 0) {  // the visit is complete: stack update
       pending = false;
-      if (shrink) {
-        tmax_f = f32_round_up(closest);
-        tmax_x = tmax_f * 1.00001f;
-#pragma unroll
-        for (int c = 0; c < 4; c++)
-          if (tt[c] > tmax_f) tt[c] = __builtin_inff();
-      }
-      cswap4(tt[0], cc[0], tt[1], cc[1]);
-      cswap4(tt[2], cc[2], tt[3], cc[3]);
-      cswap4(tt[0], cc[0], tt[2], cc[2]);
-      cswap4(tt[1], cc[1], tt[3], cc[3]);
-      cswap4(tt[1], cc[1], tt[2], cc[2]);
-      if (tt[0] != __builtin_inff()) {
-        // branchless pushes, as in trace4_run
-#pragma unroll
-        for (int c = 3; c >= 1; c--) {
-          stk[sp * stride] = (uint32_t)cc[c];
-          sp += tt[c] != __builtin_inff() ? 1 : 0;
-        }
-        node = (uint32_t)cc[0];
-      } else {
-        if (sp == 0) break;
-        node = stk[(--sp) * stride];
-      }
+      if (!visit_next<STACK>(tt, cc, shrink, closest, tmax_f, tmax_x, stk, stride, sp, node)) break;
     }
   }
   ts.node = node, ts.sp = sp, ts.closest = closest, ts.best = best, ts.mat = mat_best, ts.tmax_f = tmax_f;
@@ -1340,12 +1287,8 @@ __device__ __forceinline__ bool trace4_run_step(const DScene& S, V3 o, V3 d, dou
 
 template <int STACK, bool COUNT, int KIND = -1>
 __device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double tmin, uint32_t* stk, int stride,
-                                           Counters& cnt, TravState& ts, int park_at, uint32_t* pool = nullptr) {
-#ifndef RTX_POOL_REMAT
-#define RTX_POOL_REMAT 1
-#endif
-  if (RTX_LEAF_STEP && !(RTX_LEAF_POOL && pool))
-    return trace4_run_step<STACK, COUNT, KIND>(S, o, d, tmin, stk, stride, cnt, ts, park_at);
+                                           Counters& cnt, TravState& ts, int park_at) {
+  if (RTX_LEAF_STEP) return trace4_run_step<STACK, COUNT, KIND>(S, o, d, tmin, stk, stride, cnt, ts, park_at);
   FRay4L r = make_fray4l(o, d);
   const char* __restrict__ nbase = (const char*)S.f4nodes;
   double closest = ts.closest, t;
@@ -1360,7 +1303,6 @@ __device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double t
       done = false;
       break;
     }
-    const uint32_t noff = node << 7;  // sizeof(F4Node) == 128
     if (COUNT) {
       cnt.nodes++;
       if (first_active_lane()) cnt.wnodes++;
@@ -1370,51 +1312,9 @@ __device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double t
         for (int i = 0; i < 6; i++) cnt.tail[i] += act <= (1 << i) ? 1u : 0u;
 #endif
     }
-    const int4 ch = *(const int4*)(nbase + (noff + 96u));
-    const float4 ex = *(const float4*)(nbase + (noff + r.ox)), fx = *(const float4*)(nbase + (noff + (r.ox ^ 16u)));
-    const float4 ey = *(const float4*)(nbase + (noff + r.oy)), fy = *(const float4*)(nbase + (noff + (r.oy ^ 16u)));
-    const float4 ez = *(const float4*)(nbase + (noff + r.oz)), fz = *(const float4*)(nbase + (noff + (r.oz ^ 16u)));
     float tt[4];
-    int32_t cc[4] = {ch.x, ch.y, ch.z, ch.w};
-    uint32_t lmask = 0;
-#if RTX_PK_SLAB
-    // the 24 plane distances as 12 packed FMAs (v_pk_fma_f32: two children per instruction,
-    // the ray's per-axis constants broadcast); same single-rounding fma per plane as below
-    float pe[3][4], pf[3][4];
-    {
-      const float4 E[3] = {ex, ey, ez}, F[3] = {fx, fy, fz};
-      const pk2 en[3] = {pk2{r.iex, r.nex}, pk2{r.iey, r.ney}, pk2{r.iez, r.nez}};
-      const pk2 xn[3] = {pk2{r.ixx, r.nxx}, pk2{r.ixy, r.nxy}, pk2{r.ixz, r.nxz}};
-#pragma unroll
-      for (int a = 0; a < 3; a++) {
-        const pk2 e01 = pk_fma_bcast(pk2{E[a].x, E[a].y}, en[a]);
-        const pk2 e23 = pk_fma_bcast(pk2{E[a].z, E[a].w}, en[a]);
-        const pk2 f01 = pk_fma_bcast(pk2{F[a].x, F[a].y}, xn[a]);
-        const pk2 f23 = pk_fma_bcast(pk2{F[a].z, F[a].w}, xn[a]);
-        pe[a][0] = e01.x, pe[a][1] = e01.y, pe[a][2] = e23.x, pe[a][3] = e23.y;
-        pf[a][0] = f01.x, pf[a][1] = f01.y, pf[a][2] = f23.x, pf[a][3] = f23.y;
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const float tn = fmaxf(fmaxf(pe[0][c], pe[1][c]), fmaxf(pe[2][c], 0.0f));
-      const float tf = fminf(fminf(pf[0][c], pf[1][c]), fminf(pf[2][c], tmax_x));
-      const bool hit = tn <= tf;
-      lmask |= (hit && cc[c] < 0) ? (1u << c) : 0u;
-      tt[c] = (hit && cc[c] >= 0) ? tn : __builtin_inff();
-    }
-#else
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const float tn = fmaxf(fmaxf(fmaf(f4c(ex, c), r.iex, r.nex), fmaf(f4c(ey, c), r.iey, r.ney)),
-                             fmaxf(fmaf(f4c(ez, c), r.iez, r.nez), 0.0f));
-      const float tf = fminf(fminf(fmaf(f4c(fx, c), r.ixx, r.nxx), fmaf(f4c(fy, c), r.ixy, r.nxy)),
-                             fminf(fmaf(f4c(fz, c), r.ixz, r.nxz), tmax_x));
-      const bool hit = tn <= tf;
-      lmask |= (hit && cc[c] < 0) ? (1u << c) : 0u;
-      tt[c] = (hit && cc[c] >= 0) ? tn : __builtin_inff();
-    }
-#endif
+    int32_t cc[4];
+    uint32_t lmask = visit_slabs(nbase, node, r, tmax_x, tt, cc);
 #if RTX_TAILHIST
     if (COUNT) {
       const int nl = __popc(lmask);
@@ -1424,26 +1324,12 @@ __device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double t
       cnt.leaft += nl;
     }
 #endif
-    bool pooled = false, shrink = false;
-    if (RTX_LEAF_POOL && pool) {
-      pooled = __ballot(__popc(lmask) >= 2) != 0;  // wave-uniform
-      if (pooled) {
-        pooled_leaf_tests<KIND>(S, o, d, tmin, lmask, cc, pool, cnt, COUNT, closest, best, mat_best, shrink);
-#if RTX_POOL_REMAT
-        // the slab constants are recomputed from (o, d) after the pooled tests rather than held
-        // across them (the opaque pins keep the compiler from reusing the old values)
-        pin(o);
-        pin(d);
-        r = make_fray4l(o, d);
-#endif
-      }
-    }
     if (lmask) {
-      while (lmask && !pooled) {
+      bool shrink = false;
+      while (lmask) {  // the visit's leaf slots, in slot order
         const int c = __builtin_ctz(lmask);
         lmask &= lmask - 1u;
-        const int32_t c01 = (c & 1) ? cc[1] : cc[0], c23 = (c & 1) ? cc[3] : cc[2];
-        const uint32_t cur = ~(uint32_t)((c & 2) ? c23 : c01);
+        const uint32_t cur = leaf_prim(cc, c);
         if (COUNT) {
           count_prim(cnt, S.prims + cur);
           if (first_active_lane()) cnt.wprims++;
@@ -1451,7 +1337,7 @@ __device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double t
         if (prim_t<KIND>(S.prims + cur, S.has_tris, o, d, tmin, closest, t, m))
           closest = t, best = (int32_t)cur, mat_best = m, shrink = true;
       }
-      if (shrink) {
+      if (shrink) {  // children entered beyond the new closest hit are dropped
         tmax_f = f32_round_up(closest);
         tmax_x = tmax_f * 1.00001f;
 #pragma unroll
@@ -1459,38 +1345,9 @@ __device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double t
           if (tt[c] > tmax_f) tt[c] = __builtin_inff();
       }
     }
-    cswap4(tt[0], cc[0], tt[1], cc[1]);
-    cswap4(tt[2], cc[2], tt[3], cc[3]);
-    cswap4(tt[0], cc[0], tt[2], cc[2]);
-    cswap4(tt[1], cc[1], tt[3], cc[3]);
-    cswap4(tt[1], cc[1], tt[2], cc[2]);
-    if (tt[0] != __builtin_inff()) {
-#if RTX_PUSH_BRANCHLESS
-      // The sort leaves the entered children as a prefix (the others carry +inf and sort
-      // last), so the pushes are unconditional stores at sp, with sp advanced only for an
-      // entered child: the store of a child not entered is overwritten by the next one or
-      // lies just above the stack top.  build_fast4 bounds sp by the tree's exact worst case
-      // (need <= STACK, checked on the host), so every store index is <= STACK and the
-      // kernels give each lane STACK + 1 slots (stack_lds_bytes).
-#pragma unroll
-      for (int c = 3; c >= 1; c--) {
-        stk[sp * stride] = (uint32_t)cc[c];
-        sp += tt[c] != __builtin_inff() ? 1 : 0;
-      }
-#else
-#pragma unroll
-      for (int c = 3; c >= 1; c--) {
-        if (tt[c] != __builtin_inff()) {
-          if (sp + 1 > STACK) __builtin_trap();
-          stk[(sp++) * stride] = (uint32_t)cc[c];
-        }
-      }
-#endif
-      node = (uint32_t)cc[0];
-    } else {
-      if (sp == 0) break;
-      node = stk[(--sp) * stride];
-    }
+    // (visit_next without its shrink step: this loop's own layout of the same operations
+    // schedules better for the plain kernel, ab_refac_*)
+    if (!visit_next<STACK>(tt, cc, false, closest, tmax_f, tmax_x, stk, stride, sp, node)) break;
   }
   ts.node = node, ts.sp = sp, ts.closest = closest, ts.best = best, ts.mat = mat_best, ts.tmax_f = tmax_f;
   return done;
@@ -1516,13 +1373,13 @@ __device__ __forceinline__ int64_t trace_flat(const DScene& S, V3 o, V3 d, doubl
 template <int STACK, bool COUNT, int KIND = -1>
 __device__ __forceinline__ int64_t trace_fast4_lean(const DScene& S, V3 o, V3 d, double tmin, double tmax,
                                                     uint32_t* stk, int stride, Counters& cnt, double& t_best,
-                                                    int32_t& mat_best, uint32_t* pool = nullptr) {
+                                                    int32_t& mat_best) {
   // KIND >= 0 builds run only on scenes with a fast tree (an internal root): no flat list
   if (KIND < 0 && (!S.use_bvh || S.froot_leaf)) return trace_flat(S, o, d, tmin, tmax, cnt, COUNT, t_best, mat_best);
   TravState ts;
   trav_init(ts, tmax);
   trav_globals<COUNT>(S, o, d, tmin, cnt, ts);
-  trace4_run<STACK, COUNT, KIND>(S, o, d, tmin, stk, stride, cnt, ts, -1, pool);
+  trace4_run<STACK, COUNT, KIND>(S, o, d, tmin, stk, stride, cnt, ts, -1);
   t_best = ts.closest, mat_best = ts.mat;
   return ts.best;
 }

@@ -141,19 +141,16 @@ constexpr size_t stack_lds_bytes(int STACK) { return (size_t)(STACK + 1) * kBloc
 // origin, so both stay in LDS while the lane walks the tree and samples the BSDF instead of
 // occupying 12 of the 128 VGPRs a lane has at 4 waves per SIMD (or spilling to scratch).
 constexpr int kLdsThr = RTX_THR_LDS ? 3 : 0, kLdsHitP = RTX_HITP_LDS ? 3 : 0;
-// ... and the pooled leaf tests' candidate lists (RTX_LEAF_POOL): kPoolWords per wave
-constexpr size_t kLdsPool = RTX_LEAF_POOL ? (size_t)(kBlock / 64) * kPoolWords * sizeof(uint32_t) : 0;
 constexpr size_t persistent_lds_bytes(int stack_slots) {
-  return (size_t)stack_slots * kBlock * sizeof(uint32_t) + (size_t)(kLdsThr + kLdsHitP) * kBlock * sizeof(double) +
-         kLdsPool;
+  return (size_t)stack_slots * kBlock * sizeof(uint32_t) + (size_t)(kLdsThr + kLdsHitP) * kBlock * sizeof(double);
 }
 
 template <int STACK, bool FAST, bool COUNT, int TK = -1>
 __device__ __forceinline__ int64_t trace(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
-                                         Counters& c, double& t_best, int32_t& mat_best, uint32_t* pool = nullptr) {
+                                         Counters& c, double& t_best, int32_t& mat_best) {
 #if RTX_BVH4
 #if RTX_NODE_LEAN
-  if (FAST) return trace_fast4_lean<STACK, COUNT, TK>(S, o, d, tmin, tmax, stk, kBlock, c, t_best, mat_best, pool);
+  if (FAST) return trace_fast4_lean<STACK, COUNT, TK>(S, o, d, tmin, tmax, stk, kBlock, c, t_best, mat_best);
 #else
   if (FAST) return trace_fast4<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best, mat_best);
 #endif
@@ -352,11 +349,6 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
   // nothing else reads rec.p (textured builds: once the texture lookups moved before the sampling)
   constexpr bool kHitpLds = RTX_HITP_LDS && (NOTEX || RTX_EARLY_TEX) && !SCATTER && RTX_MERGED_SHADE;
   (void)hitp_lds;
-  // this wave's pooled-leaf-test list (after the throughput and hit-point areas)
-  uint32_t* pool = (FAST && RTX_LEAF_POOL && A.S.pool_ok)
-                       ? (uint32_t*)(lds + A.stack_slots * kBlock + 2 * (kLdsThr + kLdsHitP) * kBlock) +
-                             (threadIdx.x >> 6) * kPoolWords
-                       : nullptr;
   const uint64_t nslots = (uint64_t)A.npix * (uint64_t)A.K;
   // GetPixel uses Interval(0.001, inf) (camera.h:158); IntersectBatch uses 0.001f (cpu_ray_integrator.h:21)
   const double tmin = SCATTER ? 0.001 : (double)0.001f;
@@ -491,14 +483,14 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
         }
         // parking only when some lane of this round finishes first: every round makes progress
         const bool done = trace4_run<STACK, COUNT, TK>(A.S, P.o, P.d, tmin, stk, kBlock, c, trs,
-                                                   active > RTX_PARK ? RTX_PARK : -1, pool);
+                                                   active > RTX_PARK ? RTX_PARK : -1);
         parked = !done;
         if (parked) continue;
         best = trs.best, tb = trs.closest, bmat = trs.mat;
       } else if (kPark) {  // no BVH, or its root is a leaf
         best = trace_flat(A.S, P.o, P.d, tmin, kInf, c, COUNT, tb, bmat);
       } else {
-        best = trace<STACK, FAST, COUNT, TK>(A.S, P.o, P.d, tmin, kInf, stk, c, tb, bmat, pool);
+        best = trace<STACK, FAST, COUNT, TK>(A.S, P.o, P.d, tmin, kInf, stk, c, tb, bmat);
       }
       RTX_STAMP(1)
       segs++;
