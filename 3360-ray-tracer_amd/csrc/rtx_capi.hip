@@ -103,7 +103,10 @@ struct BandSink {
   int (*copy)(void* ctx, int64_t p0, int64_t p1, hipStream_t cs);
   void* ctx;
 };
-constexpr int kBands = 4;
+#ifndef RTX_BANDS
+#define RTX_BANDS 8  // bands of the last accumulate and of the D2H copies that overlap them (ab_bands_*: 2 / 4 / 8 / 16)
+#endif
+constexpr int kBands = RTX_BANDS;
 
 struct rtx_scene {
   int device = 0;
