@@ -24,6 +24,9 @@ CASES = [  # scene recipe, camera preset, width, spp, depth, mode, precision, ad
     ("final", "c2_final", 64, 8, 50, "wavefront", "fast", False),
     ("final", "c2_final", 48, 100, 50, "persistent", "fast", False),  # many accumulate chunks
     ("bunny", "c3_bunny", 48, 37, 20, "persistent", "fast", False),  # odd K: unaligned runs
+    ("bunny", "c3_bunny", 160, 16, 20, "persistent", "fast", False, "park"),  # the PARK kernel, forced
+    ("mixed", "c5_mixed", 96, 8, 50, "persistent", "fast", False, "park"),
+    ("cornell", "cornell", 64, 16, 50, "persistent", "fast", False, "park"),
 ]
 
 
@@ -34,10 +37,11 @@ def child(out):
     import rtx
 
     res = {}
-    for i, (scene, preset, w, spp, depth, mode, prec, adaptive) in enumerate(CASES):
+    for i, (scene, preset, w, spp, depth, mode, prec, adaptive, *sched) in enumerate(CASES):
         dev = rtx.DeviceScene(rtx.HostScene.recipe(scene, 1234), device=0)
         cam = rtx.camera(rtx.camera_config(preset, width=w))
-        rgb, n, st = dev.render(cam, spp, depth, seed=1234, adaptive=adaptive, mode=mode, precision=prec)
+        rgb, n, st = dev.render(cam, spp, depth, seed=1234, adaptive=adaptive, mode=mode, precision=prec,
+                                **({"schedule": sched[0]} if sched else {}))
         res[f"rgb{i}"], res[f"spp{i}"] = rgb, n
         res[f"rays{i}"] = np.array([st["rays_total"]])
     np.savez(out, **res)
