@@ -117,6 +117,7 @@ struct rtx_scene {
   DScene S{};
   int stack_parity = 32, stack_fast = 32;
   int fast_need = 0;     // exact worst-case stack depth of the lean BVH4 walk (build_fast4)
+  size_t n_f4 = 0;       // F4Node count of the fast tree
   bool fast_ok = false;  // RTX_PREC_FAST available (BVH with an internal root)
   int park = -1;         // persistent fast schedule: -1 not yet timed, 0 plain kernel, 1 PARK kernel
   DevBuf calib_rgb;      // output of the schedule-timing renders
@@ -581,7 +582,7 @@ template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK, boo
           bool NODOF = false>
 int run_persistent_k0(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
   if (A.stack_slots < 1 || A.stack_slots > STACK + 1) return fail(RTX_ERR_INVALID, "bad traversal stack size");
-  const size_t lds = persistent_lds_bytes(A.stack_slots);
+  const size_t lds = persistent_lds_bytes(A.stack_slots, PARK);
   const int grid = persistent_grid(
       L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF>, lds);
   L.build = (PARK ? RTX_BUILD_PARK : 0u) | (TK == (int)RTX_PRIM_SPHERE ? RTX_BUILD_SPHERE_TREE : 0u) |
@@ -824,6 +825,7 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
 #endif
       sc->stack_fast = need < 0 ? -1 : (need <= 32 ? 32 : (need <= 64 ? 64 : -1));
       sc->fast_need = need;
+      sc->n_f4 = f4.size();
       if (sc->stack_fast > 0 && (rc = upload(sc->fnodes, f4.data(), f4.size(), s))) return rc;
 #else
       build_fast(d->nodes, d->n_nodes, fn);
@@ -1009,6 +1011,8 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
       if (sc->park < 0 && (rc = time_park_schedule(sc, cam, prm, s))) return rc;
       L.park = sc->park == 1;
     }
+    // the speculative PARK walk keeps 16-bit node indices on its stack
+    if (RTX_LEAF_SPEC > 0 && sc->n_f4 > 65536) L.park = false;
   }
 
   // samples in flight per pixel (group size K)

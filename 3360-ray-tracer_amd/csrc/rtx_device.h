@@ -1180,9 +1180,9 @@ __device__ __forceinline__ uint32_t leaf_prim(const int32_t (&cc)[4], int c) {
 // stores at sp are unconditional and sp advances per entered child; build_fast4 bounds sp by
 // the tree's exact worst case, and the kernels give each lane STACK + 1 slots), or the stack
 // is popped.  false: the stack was empty, the walk is over.
-template <int STACK>
+template <int STACK, typename SE = uint32_t>
 __device__ __forceinline__ bool visit_next(float (&tt)[4], int32_t (&cc)[4], bool shrink, double closest,
-                                           float& tmax_f, float& tmax_x, uint32_t* stk, int stride, int& sp,
+                                           float& tmax_f, float& tmax_x, SE* stk, int stride, int& sp,
                                            uint32_t& node) {
   if (shrink) {
     tmax_f = f32_round_up(closest);
@@ -1200,7 +1200,7 @@ __device__ __forceinline__ bool visit_next(float (&tt)[4], int32_t (&cc)[4], boo
 #if RTX_PUSH_BRANCHLESS
 #pragma unroll
     for (int c = 3; c >= 1; c--) {
-      stk[sp * stride] = (uint32_t)cc[c];
+      stk[sp * stride] = (SE)cc[c];
       sp += tt[c] != __builtin_inff() ? 1 : 0;
     }
 #else
@@ -1216,7 +1216,7 @@ __device__ __forceinline__ bool visit_next(float (&tt)[4], int32_t (&cc)[4], boo
     return true;
   }
   if (sp == 0) return false;
-  node = stk[(--sp) * stride];
+  node = (uint32_t)stk[(--sp) * stride];
   return true;
 }
 
@@ -1280,6 +1280,97 @@ __device__ __forceinline__ bool trace4_run_step(const DScene& S, V3 o, V3 d, dou
       pending = false;
       if (!visit_next<STACK>(tt, cc, shrink, closest, tmax_f, tmax_x, stk, stride, sp, node)) break;
     }
+  }
+  ts.node = node, ts.sp = sp, ts.closest = closest, ts.best = best, ts.mat = mat_best, ts.tmax_f = tmax_f;
+  return done;
+}
+
+#ifndef RTX_LEAF_SPEC
+// PARK kernel: capacity of each lane's leaf queue in LDS for the speculative walk
+// (trace4_run_spec, a power of two >= 8); 0: the leaf-step walk
+#define RTX_LEAF_SPEC 0
+#endif
+#ifndef RTX_LEAF_SPEC_MIN
+#define RTX_LEAF_SPEC_MIN 24  // speculative walk: queued leaves are tested once this many lanes hold some
+#endif
+#ifndef RTX_LEAF_SPEC_WAIT
+#define RTX_LEAF_SPEC_WAIT 0  // 1: lanes that cannot visit wait for the leaf round instead of forcing it
+#endif
+// The lean walk with speculative node visits (Aila & Laine 2009, "speculative traversal"):
+// a visit's leaf slots go into the lane's FIFO queue (an LDS column of RTX_LEAF_SPEC words)
+// and the lane walks on; a wave runs leaf tests only when RTX_LEAF_SPEC_MIN lanes hold queued
+// leaves, or some lane cannot go on (its queue might overflow on the next visit, or its walk
+// is over), and then every lane with a queued leaf tests one.  Same result, bit for bit, as
+// trace4_run: the queue keeps the primitive tests in the order of the visits that found them,
+// and node visits keep their depth-first order, because an entry distance does not depend on
+// the closest hit.  A visit made before earlier leaves were tested culls its children against
+// a looser closest distance, so the walk may visit extra nodes and test extra primitives —
+// but each such primitive lies beyond a box entry the reference walk found past its closest
+// hit (f32 box entry <= the primitive's t), so it is rejected and the closest hit, winner and
+// tie order are unchanged.  A lane parks only with an empty queue, between visits.  The stack
+// holds 16-bit node indices (the host runs this kernel only on trees under 2^16 nodes), so
+// stack and queue fit the LDS of four blocks per CU.
+template <int STACK, bool COUNT, int KIND = -1>
+__device__ __forceinline__ bool trace4_run_spec(const DScene& S, V3 o, V3 d, double tmin, uint16_t* stk,
+                                                uint32_t* lq, int stride, Counters& cnt, TravState& ts,
+                                                int park_at) {
+  constexpr uint32_t F = RTX_LEAF_SPEC > 0 ? RTX_LEAF_SPEC : 8;
+  static_assert(F >= 8 && (F & (F - 1)) == 0, "leaf queue: a power of two >= 8");
+  FRay4L r = make_fray4l(o, d);
+  const char* __restrict__ nbase = (const char*)S.f4nodes;
+  double closest = ts.closest, t;
+  int32_t best = ts.best, mat_best = ts.mat, m;
+  float tmax_f = ts.tmax_f;
+  float tmax_x = tmax_f * 1.00001f;
+  int sp = ts.sp;
+  uint32_t node = ts.node;
+  bool walking = true, done = true;
+  uint32_t qh = 0, qn = 0;  // queue head and length
+  float tt[4];
+  int32_t cc[4];
+  while (true) {
+    const bool park = park_at >= 0 && __popcll(__ballot(1)) <= park_at;
+    if (park && qn == 0) {  // walking here: a lane whose walk is over has left the loop
+      done = false;
+      break;
+    }
+    if (walking && !park && qn <= F - 4) {  // a node visit; its leaf slots are queued
+      if (COUNT) {
+        cnt.nodes++;
+        if (first_active_lane()) cnt.wnodes++;
+      }
+      uint32_t lmask = visit_slabs(nbase, node, r, tmax_x, tt, cc);
+      while (lmask) {
+        lq[((qh + qn) & (F - 1)) * stride] = leaf_prim(cc, __builtin_ctz(lmask));
+        lmask &= lmask - 1u;
+        qn++;
+      }
+      walking = visit_next<STACK, uint16_t>(tt, cc, false, closest, tmax_f, tmax_x, stk, stride, sp, node);
+    }
+#if RTX_LEAF_SPEC_WAIT
+    // a lane that cannot visit waits; leaves are tested once enough lanes hold some, or no
+    // lane of the wave can visit a node any more
+    const bool can_visit = walking && !park && qn <= F - 4;
+    if (__ballot(can_visit) == 0 || __popcll(__ballot(qn != 0)) >= RTX_LEAF_SPEC_MIN) {
+#else
+    const bool blocked = qn != 0 && (!walking || park || qn > F - 4);
+    if (__ballot(blocked) != 0 || __popcll(__ballot(qn != 0)) >= RTX_LEAF_SPEC_MIN) {
+#endif
+      if (qn != 0) {  // one queued leaf, in visit order
+        const uint32_t cur = lq[qh * stride];
+        qh = (qh + 1) & (F - 1), qn--;
+        if (COUNT) {
+          count_prim(cnt, S.prims + cur);
+          if (first_active_lane()) cnt.wprims++;
+        }
+        if (prim_t<KIND>(S.prims + cur, S.has_tris, o, d, tmin, closest, t, m)) {
+          closest = t, best = (int32_t)cur, mat_best = m;
+          tmax_f = f32_round_up(closest);
+          tmax_x = tmax_f * 1.00001f;
+        }
+      }
+    }
+    if (!walking && qn == 0) break;
   }
   ts.node = node, ts.sp = sp, ts.closest = closest, ts.best = best, ts.mat = mat_best, ts.tmax_f = tmax_f;
   return done;

@@ -141,8 +141,13 @@ constexpr size_t stack_lds_bytes(int STACK) { return (size_t)(STACK + 1) * kBloc
 // origin, so both stay in LDS while the lane walks the tree and samples the BSDF instead of
 // occupying 12 of the 128 VGPRs a lane has at 4 waves per SIMD (or spilling to scratch).
 constexpr int kLdsThr = RTX_THR_LDS ? 3 : 0, kLdsHitP = RTX_HITP_LDS ? 3 : 0;
-constexpr size_t persistent_lds_bytes(int stack_slots) {
-  return (size_t)stack_slots * kBlock * sizeof(uint32_t) + (size_t)(kLdsThr + kLdsHitP) * kBlock * sizeof(double);
+// The PARK kernel with the speculative walk (RTX_LEAF_SPEC) keeps 16-bit stack entries and
+// adds each lane's leaf queue, RTX_LEAF_SPEC words, after the hit point.
+constexpr size_t persistent_lds_bytes(int stack_slots, bool park = false) {
+  const bool spec = park && RTX_LEAF_SPEC > 0;
+  return (size_t)stack_slots * kBlock * (spec ? sizeof(uint16_t) : sizeof(uint32_t)) +
+         (size_t)(kLdsThr + kLdsHitP) * kBlock * sizeof(double) +
+         (spec ? (size_t)RTX_LEAF_SPEC * kBlock * sizeof(uint32_t) : 0);
 }
 
 template <int STACK, bool FAST, bool COUNT, int TK = -1>
@@ -343,9 +348,16 @@ template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK = -1
           bool NOTEX = false, bool NODOF = false>
 __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderArgs A, unsigned long long* next_slot) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  // the speculative PARK walk's layout (= persistent_lds_bytes(.., PARK) for every launched PARK build:
+  // the host launches PARK kernels only for fast, non-scatter renders)
+  constexpr bool kSpecLds = PARK && FAST && !SCATTER && RTX_BVH4 && RTX_NODE_LEAN && RTX_PARK > 0 && RTX_LEAF_SPEC > 0;
   uint32_t* stk = lds + threadIdx.x;
-  double* thr_lds = (double*)(lds + A.stack_slots * kBlock) + threadIdx.x;  // [c * kBlock] (RTX_THR_LDS)
-  double* hitp_lds = thr_lds + kLdsThr * kBlock;                             // [c * kBlock] (RTX_HITP_LDS)
+  uint16_t* stk16 = (uint16_t*)lds + threadIdx.x;  // (kSpecLds)
+  (void)stk16;
+  double* thr_lds = (double*)(lds + A.stack_slots * (kSpecLds ? kBlock / 2 : kBlock)) + threadIdx.x;  // [c * kBlock]
+  double* hitp_lds = thr_lds + kLdsThr * kBlock;  // [c * kBlock] (RTX_HITP_LDS)
+  uint32_t* leafq = (uint32_t*)(hitp_lds - threadIdx.x + kLdsHitP * kBlock) + threadIdx.x;  // (kSpecLds)
+  (void)leafq;
   // nothing else reads rec.p (textured builds: once the texture lookups moved before the sampling)
   constexpr bool kHitpLds = RTX_HITP_LDS && (NOTEX || RTX_EARLY_TEX) && !SCATTER && RTX_MERGED_SHADE;
   (void)hitp_lds;
@@ -482,8 +494,11 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
           trav_globals<COUNT>(A.S, P.o, P.d, tmin, c, trs);
         }
         // parking only when some lane of this round finishes first: every round makes progress
-        const bool done = trace4_run<STACK, COUNT, TK>(A.S, P.o, P.d, tmin, stk, kBlock, c, trs,
-                                                   active > RTX_PARK ? RTX_PARK : -1);
+        const bool done =
+            kSpecLds ? trace4_run_spec<STACK, COUNT, TK>(A.S, P.o, P.d, tmin, stk16, leafq, kBlock, c, trs,
+                                                         active > RTX_PARK ? RTX_PARK : -1)
+                     : trace4_run<STACK, COUNT, TK>(A.S, P.o, P.d, tmin, stk, kBlock, c, trs,
+                                                    active > RTX_PARK ? RTX_PARK : -1);
         parked = !done;
         if (parked) continue;
         best = trs.best, tb = trs.closest, bmat = trs.mat;
