@@ -16,6 +16,7 @@
 #include "rtx.h"
 #include "rtx_kernels.h"
 #include "rtx_p3.h"
+#include "rtx_scan.h"
 
 using namespace rtxd;
 
@@ -103,10 +104,26 @@ struct BandSink {
   int (*copy)(void* ctx, int64_t p0, int64_t p1, hipStream_t cs);
   void* ctx;
 };
-#ifndef RTX_BANDS
-#define RTX_BANDS 8  // bands of the last accumulate and of the D2H copies that overlap them (ab_bands_*: 2 / 4 / 8 / 16)
-#endif
-constexpr int kBands = RTX_BANDS;
+constexpr int kBands = 8;  // bands of the last accumulate and of the D2H copies that overlap them (ab_bands_*: 2 / 4 / 8 / 16)
+
+// Adaptive renders in phases (render_adaptive): the pixels are split into kAdaptSubs
+// interleaved sub-renders, each with its own workspace and stream, so one sub-render's
+// phase-end work (the launch tail, the record / scan / expand kernels, the host's look at the
+// next phase's size) overlaps the other's tracing.
+constexpr int kAdaptSubs = 2;
+struct AdaptWs {
+  DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then the slot count (u64)
+  HostBuf total_h;                              // pinned copy of the next phase's slot count
+  hipStream_t st = nullptr;                     // sub-render 0 runs on the caller's stream
+  hipEvent_t ev = nullptr;                      // total_h written
+  void release() {
+    for (DevBuf* b : {&lbuf, &smap, &k[0], &k[1], &off, &scan_tmp, &ctr}) b->release();
+    total_h.release();
+    if (ev) (void)hipEventDestroy(ev);
+    if (st) (void)hipStreamDestroy(st);
+    ev = nullptr, st = nullptr;
+  }
+};
 
 struct rtx_scene {
   int device = 0;
@@ -131,7 +148,14 @@ struct rtx_scene {
   // banded output copies (BandSink): a copy stream and its ordering events
   hipStream_t copy_stream = nullptr;
   std::vector<hipEvent_t> band_ev;
+  AdaptWs aw[kAdaptSubs];
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  double slot_mem = -1.0;  // bytes the slot buffers may take (slot_target; -1: not yet queried)
   ~rtx_scene() {
+    (void)hipSetDevice(device);
+    for (auto& w : aw) w.release();
+    for (hipEvent_t e : {fork_ev, join_ev})
+      if (e) (void)hipEventDestroy(e);
     for (auto e : evpool) (void)hipEventDestroy(e);
     for (auto e : band_ev) (void)hipEventDestroy(e);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
@@ -163,33 +187,6 @@ int bvh_depth(const rtx_bvh_node* n, int64_t count) {
     }
   }
   return m;
-}
-
-// BVH2 fast layout: one FNode per internal node, holding both children's outward-rounded
-// f32 boxes (see rtx_device.h FNode / fbox).
-[[maybe_unused]] void build_fast(const rtx_bvh_node* n, int64_t count, std::vector<FNode>& out) {
-  std::vector<int32_t> fidx(count, -1);
-  int32_t k = 0;
-  for (int64_t i = 0; i < count; i++)
-    if (!n[i].is_leaf) fidx[i] = k++;
-  out.assign(k, FNode{});
-  for (int64_t i = 0; i < count; i++) {
-    if (n[i].is_leaf) continue;
-    FNode& f = out[fidx[i]];
-    const uint32_t ch[2] = {n[i].left_first, n[i].right_count};
-    for (int c = 0; c < 2; c++) {
-      const rtx_bvh_node& cn = n[ch[c]];
-      float* lo = c == 0 ? f.lo0 : f.lo1;
-      float* hi = c == 0 ? f.hi0 : f.hi1;
-      for (int a = 0; a < 3; a++) lo[a] = round_down(cn.lo[a]), hi[a] = round_up(cn.hi[a]);
-      int32_t ref;
-      uint16_t cnt;
-      if (cn.is_leaf) ref = ~(int32_t)cn.left_first, cnt = (uint16_t)cn.right_count;
-      else ref = fidx[ch[c]], cnt = 0;
-      if (c == 0) f.c0 = ref, f.n0 = cnt;
-      else f.c1 = ref, f.n1 = cnt;
-    }
-  }
 }
 
 // Conservative f64 box of one primitive (fast-path leaf splitting).  Spheres: centre +-
@@ -351,7 +348,7 @@ int build_fast4(const rtx_bvh_node* n, const rtx_prim* prims, std::vector<F4Node
   return need;
 }
 
-// Fast-path tree of our own (RTX_FAST_TREE = 1): binned SAH on all three axes (32 bins)
+// Fast-path tree of our own: binned SAH on all three axes (32 bins)
 // over the conservative primitive boxes (prim_box), split down to one primitive per leaf;
 // the result uses the reference node layout (pre-order, leaf = one primitive by its index
 // in the scene's prim array) so build_fast4 collapses it like the reference tree.  The
@@ -453,12 +450,8 @@ static void build_own_sah(const rtx_prim* prims, int64_t n, const int32_t* skip,
 // primitives' boxes, i.e. a box that nearly every ray's walk would enter at the root anyway
 // (the ground spheres of the final, bunny and mixed scenes: r = 1000 against a scene a few
 // tens of units wide).  At least two primitives stay in the tree so its root is internal.
-#ifndef RTX_GLOBAL_PRIMS
-#define RTX_GLOBAL_PRIMS 1
-#endif
 static int build_global_prims(const rtx_prim* prims, int64_t n, int32_t out[2]) {
   int k = 0;
-  if (!RTX_GLOBAL_PRIMS) return 0;
   while (k < 2 && n - k > 2) {
     // largest remaining box, and the union of the others
     int64_t big = -1;
@@ -481,6 +474,25 @@ static int build_global_prims(const rtx_prim* prims, int64_t n, int32_t out[2]) 
     out[k++] = (int32_t)big;
   }
   return k;
+}
+
+// Slots (pixel x sample radiance records) a render keeps in flight: `want`, limited to half of
+// the device memory that is free or already held by this scene's slot buffers, so several
+// scenes on one device, or a smaller GPU, get smaller groups instead of RTX_ERR_NOMEM.
+// The free-memory query is made once per scene (the first render that sizes its slots; it
+// costs ~0.5 ms, too much per frame): scenes created later see what the earlier ones took.
+int64_t slot_target(rtx_scene* sc, int64_t bytes_per_slot, int64_t want) {
+  if (sc->slot_mem < 0) {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+      (void)hipGetLastError();
+      fr = (size_t)1 << 62;
+    }
+    double held = (double)sc->lbuf.n + (double)sc->queue[0].n + (double)sc->queue[1].n;
+    for (const AdaptWs& w : sc->aw) held += (double)w.lbuf.n + (double)w.smap.n;
+    sc->slot_mem = 0.5 * ((double)fr + held);
+  }
+  return std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)(sc->slot_mem / (double)bytes_per_slot)));
 }
 
 int pick_stack(int depth) {
@@ -547,15 +559,6 @@ int persistent_grid(rtx_scene* sc, const void* fn, size_t lds) {
   return std::max(1, per_cu) * sc->cus;
 }
 
-#ifndef RTX_NODOF_KERNEL
-#define RTX_NODOF_KERNEL 1  // texture-free plain build: no thin-lens code when the camera has no defocus
-#endif
-#ifndef RTX_NOTEX_KERNEL
-#define RTX_NOTEX_KERNEL 1  // texture-free scenes with a sphere tree: shading without texture lookups
-#endif
-#ifndef RTX_LAMB_KERNEL
-#define RTX_LAMB_KERNEL 1  // all-Lambertian scenes with a triangle tree: shading built for Lambertians only
-#endif
 
 struct Launch {
   rtx_scene* sc;
@@ -582,7 +585,7 @@ template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK, boo
           bool NODOF = false>
 int run_persistent_k0(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
   if (A.stack_slots < 1 || A.stack_slots > STACK + 1) return fail(RTX_ERR_INVALID, "bad traversal stack size");
-  const size_t lds = persistent_lds_bytes(A.stack_slots, PARK);
+  const size_t lds = persist_lds(A.stack_slots, spec_walk(PARK, FAST, SCATTER)).end;
   const int grid = persistent_grid(
       L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF>, lds);
   L.build = (PARK ? RTX_BUILD_PARK : 0u) | (TK == (int)RTX_PRIM_SPHERE ? RTX_BUILD_SPHERE_TREE : 0u) |
@@ -601,7 +604,7 @@ int run_persistent_k0(const Launch& L, const RenderArgs& A, unsigned long long* 
 // off; C2 +1.0 %; the PARK build lost 2.8 % with it, ab_nodof_*)
 template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK, bool LAMB = false, bool NOTEX = false>
 int run_persistent_k(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
-  if (NOTEX && !PARK && RTX_NODOF_KERNEL && A.cam.defocus_angle <= 0)
+  if (NOTEX && !PARK && A.cam.defocus_angle <= 0)
     return run_persistent_k0<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NOTEX && !PARK>(L, A, next_slot);
   return run_persistent_k0<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX>(L, A, next_slot);
 }
@@ -609,18 +612,17 @@ int run_persistent_k(const Launch& L, const RenderArgs& A, unsigned long long* n
 // the PARK schedule (the bunny), spheres with the plain one (the final and mixed scenes)
 template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK>
 int run_persistent(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
-  constexpr bool spec = FAST && !COUNT && !SCATTER && RTX_TREE_KIND;
+  constexpr bool spec = FAST && !COUNT && !SCATTER;
   constexpr int TK = spec ? (PARK ? (int)RTX_PRIM_TRIANGLE : (int)RTX_PRIM_SPHERE) : -1;
   if (TK >= 0 && A.S.tree_kind == TK && !L.generic) {
     // the triangle (PARK) build also comes for all-Lambertian scenes (the bunny)
-    if (TK == (int)RTX_PRIM_TRIANGLE && RTX_LAMB_KERNEL && A.S.all_lambertian) {
+    if (TK == (int)RTX_PRIM_TRIANGLE && A.S.all_lambertian) {
       constexpr bool tri = TK == (int)RTX_PRIM_TRIANGLE;
-      if (RTX_NOTEX_KERNEL && A.S.no_textures)
-        return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK, tri, tri>(L, A, next_slot);
+      if (A.S.no_textures) return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK, tri, tri>(L, A, next_slot);
       return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK, tri>(L, A, next_slot);
     }
     // the sphere (plain) build also comes for scenes that read no textures (the final scene)
-    if (TK == (int)RTX_PRIM_SPHERE && RTX_NOTEX_KERNEL && A.S.no_textures)
+    if (TK == (int)RTX_PRIM_SPHERE && A.S.no_textures)
       return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK, false, TK == (int)RTX_PRIM_SPHERE>(L, A,
                                                                                                        next_slot);
     return run_persistent_k<STACK, FAST, COUNT, SCATTER, PARK, TK>(L, A, next_slot);
@@ -644,7 +646,7 @@ int persist_s(const Launch& L, const RenderArgs& A, unsigned long long* ns) {
 }
 template <bool SCATTER>
 int persist_m(const Launch& L, const RenderArgs& A, unsigned long long* ns) {
-  if (L.fast && L.park && !SCATTER && RTX_PARK > 0)
+  if (L.fast && L.park && !SCATTER)
     return L.count ? persist_s<true, true, SCATTER, true>(L, A, ns) : persist_s<true, false, SCATTER, true>(L, A, ns);
   if (L.fast)
     return L.count ? persist_s<true, true, SCATTER, false>(L, A, ns) : persist_s<true, false, SCATTER, false>(L, A, ns);
@@ -652,6 +654,141 @@ int persist_m(const Launch& L, const RenderArgs& A, unsigned long long* ns) {
 }
 
 int time_park_schedule(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm, hipStream_t s);
+
+// Adaptive sampling in phases on the persistent kernel (rtx_kernels.h, "Adaptive sampling in
+// phases"): the reference's WavefrontRenderer::Render loop (wavefront.cc:57-225, always
+// adaptive) with the same per-pixel results.  The pixels are split into kAdaptSubs interleaved
+// sub-renders (pixel p = q * S + j) with their own workspace, the first on the caller's stream
+// `s`, the second on a stream of its own.  Each sub-render runs: phase 1, min_spp samples of
+// every pixel; then, after each phase, record + next batch sizes (k_adapt_record); before
+// each phase, prefix sum and slot map (k_adapt_expand); the host reads the next phase's
+// slot count (one pinned word) only once the other sub-render's phase is queued, so the GPU
+// works on one sub-render while the other sits between phases.  `mark` records a hot-kernel
+// timing event on a stream (before and after each persistent launch); hot_launches counts
+// them.  The caller resolves the pixels (k_resolve) once both sub-renders are done.
+template <class Mark>
+int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const rtx_render_params* prm,
+                    const PixelSoA& px, int budget, hipStream_t s, Mark mark, uint64_t& hot_launches) {
+  const int64_t npix = A.npix;
+  const int S = npix >= (1 << 16) ? kAdaptSubs : 1;
+  const int K1 = std::min(std::max(1, prm->min_spp), budget);
+  static const bool debug = std::getenv("RTX_DEBUG_ADAPT") != nullptr;  // per-phase slot counts on stderr
+  if ((int64_t)npix * K1 > 0xFFFFFFFFll) return fail(RTX_ERR_INVALID, "adaptive render: npix x min_spp above 2^32");
+  // slots per sub-render after the first phase: 24 B of radiance + 8 B of slot map each
+  const int64_t cap = std::min<int64_t>(0xFFFFFFFFll, slot_target(sc, S * 32, (1ll << kSlotTargetLog2) / S));
+  int64_t nq[kAdaptSubs];
+  int32_t kcap[kAdaptSubs];
+  int rc;
+  for (int j = 0; j < S; j++) {
+    AdaptWs& w = sc->aw[j];
+    nq[j] = (npix - j + S - 1) / S;
+    if (nq[j] * 4 > cap) return fail(RTX_ERR_NOMEM, "adaptive render: too many pixels for the device memory");
+    kcap[j] = (int32_t)std::min<int64_t>(budget, std::max<int64_t>(4, (cap / nq[j]) & ~3ll));
+    const int64_t slots = nq[j] * (int64_t)kcap[j];
+    if ((rc = w.lbuf.reserve(slots * 3 * sizeof(double)))) return rc;
+    if ((rc = w.smap.reserve(slots * sizeof(uint2)))) return rc;
+    for (DevBuf* b : {&w.k[0], &w.k[1], &w.off})
+      if ((rc = b->reserve(nq[j] * sizeof(uint32_t)))) return rc;
+    if ((rc = w.scan_tmp.reserve(std::max<size_t>(16, rtxscan::temp_bytes(nq[j]))))) return rc;
+    if ((rc = w.ctr.reserve(8 * 16 * sizeof(unsigned long long) + 64))) return rc;
+    if ((rc = w.total_h.reserve(sizeof(unsigned long long)))) return rc;
+    if (!w.ev) HIPC(hipEventCreateWithFlags(&w.ev, hipEventDisableTiming));
+    if (j > 0 && !w.st) HIPC(hipStreamCreateWithFlags(&w.st, hipStreamNonBlocking));
+  }
+  auto plan = [&](int j, hipStream_t st, const uint32_t* knext) -> int {  // prefix sum + slot map
+    AdaptWs& w = sc->aw[j];
+    const unsigned qb = (unsigned)((nq[j] + kBlock - 1) / kBlock);
+    HIPC(rtxscan::exclusive_scan_u32(knext, w.off.as<uint32_t>(), nq[j], w.scan_tmp.p, w.scan_tmp.n, st));
+    hipLaunchKernelGGL(k_adapt_expand, dim3(qb), dim3(kBlock), 0, st, knext, (const uint32_t*)w.off.as<uint32_t>(),
+                       nq[j], S, j, (const int32_t*)px.samples, w.smap.as<uint2>(),
+                       w.ctr.as<unsigned long long>() + 8 * 16);
+    HIPC(hipGetLastError());
+    return RTX_OK;
+  };
+  // record + next batch sizes of sub-render j's pixels after phase g (its slots in L: the
+  // uniform first phase's, or the phase's slot map), then the next phase's slot map and count
+  auto record = [&](int j, hipStream_t st, int g, const double* Lph) -> int {
+    AdaptWs& w = sc->aw[j];
+    AdaptPlan ap;
+    ap.kcur = g == 1 ? nullptr : w.k[g & 1].as<uint32_t>();
+    ap.off = g == 1 ? nullptr : w.off.as<uint32_t>();
+    ap.knext = w.k[(g + 1) & 1].as<uint32_t>();
+    ap.kuni = K1, ap.sub_n = S, ap.sub_j = j;
+    ap.min_spp = prm->min_spp, ap.budget = budget, ap.phase = g, ap.kcap = kcap[j];
+    ap.rel = prm->rel_threshold;
+    hipLaunchKernelGGL(k_adapt_record, dim3((unsigned)((nq[j] + kRecWave - 1) / kRecWave)), dim3(kRecWave), 0, st, px,
+                       Lph, nq[j], npix, ap);
+    HIPC(hipGetLastError());
+    int rc2;
+    if ((rc2 = plan(j, st, ap.knext))) return rc2;
+    HIPC(hipMemcpyAsync(w.total_h.p, w.ctr.as<unsigned long long>() + 8 * 16, sizeof(unsigned long long),
+                        hipMemcpyDeviceToHost, st));
+    HIPC(hipEventRecord(w.ev, st));
+    return RTX_OK;
+  };
+  // phase 1: min_spp samples of every pixel, one uniform launch over the whole render (the
+  // scene's radiance buffer)
+  {
+    if ((rc = sc->lbuf.reserve((size_t)npix * K1 * 3 * sizeof(double)))) return rc;
+    RenderArgs A1 = A;
+    A1.L = sc->lbuf.as<double>();
+    A1.conv = nullptr;
+    A1.K = K1, A1.s0 = 0, A1.smap = nullptr;
+    unsigned long long* ctr = sc->aw[0].ctr.as<unsigned long long>();
+    HIPC(hipMemsetAsync(ctr, 0, 8 * 16 * sizeof(unsigned long long), s));
+    if ((rc = mark(s))) return rc;
+    if ((rc = persist_m<false>(L, A1, ctr))) return rc;
+    if ((rc = mark(s))) return rc;
+    hot_launches++;
+  }
+  if (S > 1) {  // the sub-renders' streams start once the first phase is done
+    for (hipEvent_t* e : {&sc->fork_ev, &sc->join_ev})
+      if (!*e) HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    HIPC(hipEventRecord(sc->fork_ev, s));
+    for (int j = 1; j < S; j++) HIPC(hipStreamWaitEvent(sc->aw[j].st, sc->fork_ev, 0));
+  }
+  bool alive[kAdaptSubs] = {false, false};
+  for (int j = 0; j < S; j++) {
+    if ((rc = record(j, j == 0 ? s : sc->aw[j].st, 1, sc->lbuf.as<double>()))) return rc;
+    alive[j] = true;
+  }
+  for (int g = 2; alive[0] || alive[1]; g++) {
+    for (int j = 0; j < S; j++) {
+      if (!alive[j]) continue;
+      AdaptWs& w = sc->aw[j];
+      hipStream_t st = j == 0 ? s : w.st;
+      unsigned long long* ctr = w.ctr.as<unsigned long long>();  // 8 region counters, then the slot count
+      // this phase's slot count, computed at the end of the previous one
+      HIPC(hipEventSynchronize(w.ev));
+      const unsigned long long nsl = *(const volatile unsigned long long*)w.total_h.p;
+      if (debug) fprintf(stderr, "rtx adaptive: sub-render %d phase %d: %llu slots\n", j, g, nsl);
+      if (nsl == 0) {
+        alive[j] = false;
+        continue;
+      }
+      RenderArgs Aj = A;
+      Aj.L = w.lbuf.as<double>();
+      Aj.conv = nullptr;  // only pixels still sampling have slots
+      Aj.K = 1, Aj.s0 = 0;
+      Aj.smap = w.smap.as<uint2>();
+      Launch Lj = L;
+      Lj.s = st;
+      HIPC(hipMemsetAsync(ctr, 0, 8 * 16 * sizeof(unsigned long long), st));
+      if ((rc = mark(st))) return rc;
+      if ((rc = persist_m<false>(Lj, Aj, ctr))) return rc;
+      if ((rc = mark(st))) return rc;
+      hot_launches++;
+      if ((rc = record(j, st, g, Aj.L))) return rc;
+    }
+  }
+  if (S > 1) {  // s continues once every sub-render is done
+    for (int j = 1; j < S; j++) {
+      HIPC(hipEventRecord(sc->join_ev, sc->aw[j].st));
+      HIPC(hipStreamWaitEvent(s, sc->join_ev, 0));
+    }
+  }
+  return RTX_OK;
+}
 
 }  // namespace
 
@@ -736,7 +873,7 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   // would compute per hit.
   bool any_tri = false;
   for (int64_t i = 0; i < d->n_prims && !any_tri; i++) any_tri = d->prims[i].kind == RTX_PRIM_TRIANGLE;
-  if (RTX_TRI_NORMALS && any_tri) {
+  if (any_tri) {
     std::vector<double> tn((size_t)d->n_prims * 4, 0.0);
     for (int64_t i = 0; i < d->n_prims; i++) {
       const rtx_prim& q = d->prims[i];
@@ -753,21 +890,18 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
     if ((rc = upload(sc->tri_n, tn.data(), tn.size(), s))) return rc;
     HIPC(hipStreamSynchronize(s));  // tn is a temporary
   }
-  if (RTX_TRI_EDGES) {  // device table: triangles carry A, B - A, C - A (tri_e1 / tri_e2)
+  {  // device table: triangles carry A, B - A, C - A (tri_e1 / tri_e2)
     std::vector<rtx_prim> dp(d->prims, d->prims + d->n_prims);
     for (rtx_prim& q : dp)
       if (q.kind == RTX_PRIM_TRIANGLE)
         for (int a = 0; a < 3; a++) q.g[3 + a] = q.g[3 + a] - q.g[a], q.g[6 + a] = q.g[6 + a] - q.g[a];
     if ((rc = upload(sc->prims, dp.data(), dp.size(), s))) return rc;
     HIPC(hipStreamSynchronize(s));  // dp is a temporary: the copy must finish before it goes
-  } else if ((rc = upload(sc->prims, d->prims, d->n_prims, s))) {
-    return rc;
   }
   // Device copy of the material table: a Lambertian / DiffuseLight whose texture is a
   // SolidColor carries the colour itself (texture = -1, colour in the unused albedo field),
   // so shading skips the dependent texture-table load (mat_tex, rtx_device.h).
   std::vector<rtx_material> dmats(d->materials, d->materials + d->n_materials);
-#if RTX_MAT_SOLID_INLINE
   for (rtx_material& m : dmats) {
     if ((m.kind == RTX_MAT_LAMBERTIAN || m.kind == RTX_MAT_DIFFUSE_LIGHT) && m.texture >= 0 &&
         d->textures[m.texture].kind == RTX_TEX_SOLID) {
@@ -775,7 +909,6 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
       m.texture = -1;
     }
   }
-#endif
   // Dielectric: eta on a front-face hit (eta_i / eta_t = 1 / ri) and Schlick's r0 for
   // reflectance(c, ri) (material.cc:226-262) in the unused albedo field, computed with the same
   // IEEE double operations the kernel would perform (shade_merged, rtx_device.h).
@@ -803,7 +936,6 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   }
   if ((rc = upload(sc->images, imgs.data(), imgs.size(), s))) return rc;
   sc->n_nodes = d->nodes ? d->n_nodes : 0;
-  std::vector<FNode> fn;
   std::vector<F4Node> f4;
   int32_t global[2] = {0, 0};
   int n_global = 0;
@@ -814,23 +946,16 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
     sc->stack_fast = sc->stack_parity;
     if (sc->stack_parity < 0) return fail(RTX_ERR_INVALID, "BVH deeper than 62 levels");
     if (!d->nodes[0].is_leaf) {
-#if RTX_BVH4
-#if RTX_FAST_TREE
+      // the fast path's tree: our own binned SAH tree over the primitives (without the global
+      // ones), collapsed to BVH4 (r01: +2 % C2 / bunny, +6 % C5 over collapsing the reference's)
       std::vector<rtx_bvh_node> own;
       n_global = build_global_prims(d->prims, d->n_prims, global);
       build_own_sah(d->prims, d->n_prims, global, n_global, own);
       const int need = build_fast4(own.data(), d->prims, f4);
-#else
-      const int need = build_fast4(d->nodes, d->prims, f4);
-#endif
       sc->stack_fast = need < 0 ? -1 : (need <= 32 ? 32 : (need <= 64 ? 64 : -1));
       sc->fast_need = need;
       sc->n_f4 = f4.size();
       if (sc->stack_fast > 0 && (rc = upload(sc->fnodes, f4.data(), f4.size(), s))) return rc;
-#else
-      build_fast(d->nodes, d->n_nodes, fn);
-      if ((rc = upload(sc->fnodes, fn.data(), fn.size(), s))) return rc;
-#endif
       sc->fast_ok = sc->stack_fast > 0;
     }
   }
@@ -842,7 +967,6 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   S.mats = sc->mats.as<rtx_material>();
   S.texs = sc->texs.as<rtx_texture>();
   S.images = sc->images.as<DImage>();
-  S.fnodes = fn.empty() ? nullptr : sc->fnodes.as<FNode>();
   S.f4nodes = (f4.empty() || !sc->fast_ok) ? nullptr : sc->fnodes.as<F4Node>();
   S.use_bvh = (d->nodes && d->n_nodes > 0) ? 1 : 0;
   S.n_prims = S.use_bvh ? d->n_prims : d->n_prims;
@@ -1003,7 +1127,7 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   const bool fast = prm->precision == RTX_PREC_FAST && sc->fast_ok;
   Launch L{sc, s, fast ? sc->stack_fast : sc->stack_parity, fast, (prm->flags & RTX_FLAG_COUNT) != 0};
   L.generic = (prm->flags & RTX_FLAG_GENERIC) != 0;
-  if (fast && prm->mode == RTX_MODE_PERSISTENT && RTX_PARK > 0) {
+  if (fast && prm->mode == RTX_MODE_PERSISTENT) {
     if (prm->flags & RTX_FLAG_PARK) L.park = true;
     else if (prm->flags & RTX_FLAG_NO_PARK) L.park = false;
     else {
@@ -1011,8 +1135,13 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
       if (sc->park < 0 && (rc = time_park_schedule(sc, cam, prm, s))) return rc;
       L.park = sc->park == 1;
     }
-    // the speculative PARK walk keeps 16-bit node indices on its stack
-    if (RTX_LEAF_SPEC > 0 && sc->n_f4 > 65536) L.park = false;
+    // the speculative PARK walk keeps 16-bit node indices on its stack: larger trees get the
+    // plain kernel, and a render that asks for the PARK kernel is refused
+    if (RTX_LEAF_SPEC > 0 && sc->n_f4 > 65536) {
+      if (prm->flags & RTX_FLAG_PARK)
+        return fail(RTX_ERR_INVALID, "RTX_FLAG_PARK: the speculative PARK walk takes trees of at most 65536 nodes");
+      L.park = false;
+    }
   }
 
   // samples in flight per pixel (group size K)
@@ -1021,12 +1150,19 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     // slots in flight: each persistent launch ends in a tail of draining lanes, so fewer,
     // larger groups pay it less often (Lbuf = 24 B per slot); the wavefront's two queues cost
     // 84 B per slot each and keep the smaller target
-    const int64_t target = prm->mode == RTX_MODE_WAVEFRONT ? (1ll << 25) : (1ll << RTX_SLOT_TARGET_LOG2);
+    const int64_t target = prm->mode == RTX_MODE_WAVEFRONT
+                               ? slot_target(sc, 3 * sizeof(double) + 2 * (9 * sizeof(double) + 3 * sizeof(uint32_t)), 1ll << 25)
+                               : slot_target(sc, 3 * sizeof(double), 1ll << kSlotTargetLog2);
     K = (int)std::max<int64_t>(1, std::min<int64_t>(budget > 0 ? budget : 1, target / std::max<int64_t>(1, npix)));
   }
   K = std::max(1, std::min(K, std::max(1, budget)));
   if ((int64_t)npix * K > 0xFFFFFFFFll) return fail(RTX_ERR_INVALID, "too many slots in one group (lower samples_per_group)");
   const int64_t nslots = npix * (int64_t)K;
+
+  // the reference's default sampling (adaptive) on the persistent kernel: in phases
+  // (render_adaptive); an explicit samples_per_group keeps uniform groups
+  const bool phased = prm->mode == RTX_MODE_PERSISTENT && prm->adaptive && !mk_adaptive &&
+                      prm->samples_per_group <= 0 && budget > 0 && npix > 0;
 
   int rc;
   if ((rc = sc->px_sum.reserve(npix * 3 * sizeof(double)))) return rc;
@@ -1034,7 +1170,7 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   if ((rc = sc->px_m2.reserve(npix * 3 * sizeof(double)))) return rc;
   if ((rc = sc->px_samples.reserve(npix * sizeof(int32_t)))) return rc;
   if ((rc = sc->px_conv.reserve(npix))) return rc;
-  if ((rc = sc->lbuf.reserve(nslots * 3 * sizeof(double)))) return rc;
+  if (!phased && (rc = sc->lbuf.reserve(nslots * 3 * sizeof(double)))) return rc;
   if ((rc = sc->counters.reserve(kCounterWords * sizeof(unsigned long long)))) return rc;
   const size_t qbytes = nslots * (9 * sizeof(double) + 3 * sizeof(uint32_t));
   if (prm->mode == RTX_MODE_WAVEFRONT)
@@ -1076,13 +1212,14 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   A.conv = prm->adaptive ? sc->px_conv.as<uint8_t>() : nullptr;
   A.L = sc->lbuf.as<double>();
   A.counters = cnt;
-  // the lean BVH4 walk stores at most fast_need + 1 stack slots (RTX_PUSH_BRANCHLESS); the
+  A.smap = nullptr;
+  // the lean BVH4 walk stores at most fast_need + 1 stack slots (branchless pushes); the
   // parity walk gets its template bound (pick_stack: reference depth + 2)
-  A.stack_slots = (fast && RTX_NODE_LEAN && RTX_PUSH_BRANCHLESS) ? sc->fast_need + 1 : L.stack + 1;
-  // counters[8..] : queue counts (u32) for the wavefront, [16] slot counter (persistent);
-  // [64 + 16 g] the slot counters of the 8 regions (RTX_XCD_REGIONS), 128 bytes apart
+  A.stack_slots = fast ? sc->fast_need + 1 : L.stack + 1;
+  // counters[8..] : queue counts (u32) for the wavefront;
+  // [64 + 16 g] the slot counters of the 8 regions, 128 bytes apart
   unsigned* qcount = (unsigned*)(cnt + 8);
-  unsigned long long* next_slot = RTX_XCD_REGIONS ? cnt + 64 : cnt + 16;
+  unsigned long long* next_slot = cnt + 64;
   auto make_queue = [&](DevBuf& b) {
     PathQueue q;
     double* d = b.as<double>();
@@ -1110,7 +1247,18 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   if (timed) HIPC(hipEventRecord(sc->ev[0], s));
   const int pix_blocks = (int)((npix + kBlock - 1) / kBlock);
   const int wf_grid = std::max(1, std::min<int>(sc->cus * 16, (int)((nslots + kBlock - 1) / kBlock)));
-  for (int s0 = 0, Kc = 0; s0 < budget; s0 += Kc) {
+  if (phased) {
+    if ((rc = render_adaptive(sc, L, A, prm, px, budget, s, [&](hipStream_t st) -> int {
+           if (timed) {
+             hipEvent_t e = ev_at(evi++);
+             if (!e) return fail(RTX_ERR_HIP, "hipEventCreate failed");
+             HIPC(hipEventRecord(e, st));
+           }
+           return RTX_OK;
+         }, hot_launches)))
+      return rc;
+  }
+  for (int s0 = 0, Kc = 0; s0 < budget && !phased; s0 += Kc) {
     Kc = std::min(K, budget - s0);
     // adaptive with automatic grouping: nothing can converge before min_spp, afterwards
     // small groups limit the samples traced past a pixel's convergence point
@@ -1143,7 +1291,7 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
         hot_launches++;
       }
     } else {
-      HIPC(hipMemsetAsync(next_slot, 0, (RTX_XCD_REGIONS ? 8 * 16 : 1) * sizeof(unsigned long long), s));
+      HIPC(hipMemsetAsync(next_slot, 0, 8 * 16 * sizeof(unsigned long long), s));
       if ((rc = hot_begin())) return rc;
       rc = prm->mode == RTX_MODE_MEGAKERNEL ? persist_m<true>(L, A, next_slot) : persist_m<false>(L, A, next_slot);
       if (rc) return rc;
@@ -1220,30 +1368,7 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     stats->tri_tests = h[6];
     stats->sphere_tests = h[7];
     stats->build = prm->mode == RTX_MODE_WAVEFRONT ? 0 : L.build;
-    stats->node_bytes = (L.fast && RTX_BVH4) ? sizeof(F4Node) : (L.fast ? sizeof(FNode) : sizeof(rtx_bvh_node));
-#if RTX_TAILHIST
-    if (h[4]) {
-      unsigned long long th[6];
-      HIPC(hipMemcpy(th, cnt + 40, sizeof th, hipMemcpyDeviceToHost));
-      fprintf(stderr, "rtx tail: node-loop wave iterations %llu; fraction with <=1/2/4/8/16/32 active lanes:", h[4]);
-      for (int i = 0; i < 6; i++) fprintf(stderr, " %.4f", (double)th[i] / (double)h[4]);
-      fprintf(stderr, "\n");
-      unsigned long long lh[5];
-      HIPC(hipMemcpy(lh, cnt + 46, sizeof lh, hipMemcpyDeviceToHost));
-      const double ph = (double)(lh[0] + lh[1] + lh[2] + lh[3]);
-      fprintf(stderr, "rtx leaf: node iterations with leaf tests %.0f (%.4f of node-loop iterations); leaf-loop length "
-              "1/2/3/4: %.4f %.4f %.4f %.4f; leaf tests per such iteration %.2f; leaf-loop wave iterations %.0f\n",
-              ph, ph / (double)h[4], lh[0] / ph, lh[1] / ph, lh[2] / ph, lh[3] / ph, (double)lh[4] / ph,
-              (double)(lh[0] + 2 * lh[1] + 3 * lh[2] + 4 * lh[3]));
-    }
-#endif
-#if RTX_STAMPS
-    unsigned long long st[4];
-    HIPC(hipMemcpy(st, cnt + 24, sizeof st, hipMemcpyDeviceToHost));
-    const double tot = (double)(st[0] + st[1] + st[2] + st[3]);
-    fprintf(stderr, "rtx stamps (wave cycles): refill %.3f trace %.3f shade %.3f other %.3f total %.4g\n",
-            st[0] / tot, st[1] / tot, st[2] / tot, st[3] / tot, tot);
-#endif
+    stats->node_bytes = L.fast ? sizeof(F4Node) : sizeof(rtx_bvh_node);
   }
   return RTX_OK;
 }
@@ -1557,6 +1682,23 @@ extern "C" int rtx_internal_check_sincos(int device, int64_t n, uint64_t seed, i
   HIPC(hipMemcpy(h, bad, sizeof(h), hipMemcpyDeviceToHost));
   *mismatches = (int64_t)h[0];
   if (first_bad) std::memcpy(first_bad, &h[1], sizeof(double));
+  return RTX_OK;
+}
+
+// Test hook (not in rtx.h): the persistent kernel's LDS layout (persist_lds) for a traversal
+// stack of stack_slots entries per lane, the PARK build (park = 1: its speculative walk when
+// compiled in) or the plain one: out[0..4] = byte offsets of the stack, throughput, hit point,
+// leaf queue and the block's LDS size; out[5..8] = each region's bytes per lane (entries x
+// element size), the regions being lane-interleaved with stride kBlock.  tests/
+// test_capi_exports.py checks that the regions are disjoint and inside the block's LDS for every
+// stack size the host can choose.
+extern "C" int rtx_internal_lds_layout(int stack_slots, int park, uint32_t* out) {
+  if (stack_slots < 1 || stack_slots > 65 || !out) return fail(RTX_ERR_INVALID, "bad argument");
+  const bool spec = spec_walk(park != 0, true, false);
+  const PersistLds l = persist_lds(stack_slots, spec);
+  const uint32_t v[9] = {l.stack, l.thr, l.hitp, l.leafq, l.end, (uint32_t)stack_slots * (spec ? 2u : 4u), 24u, 24u,
+                         spec ? (uint32_t)RTX_LEAF_SPEC * 4u : 0u};
+  std::memcpy(out, v, sizeof v);
   return RTX_OK;
 }
 

@@ -12,26 +12,21 @@
 
 #include "rtx.h"
 
-#ifndef RTX_SIGNED_PLANES
-#define RTX_SIGNED_PLANES 1  // A/B r01: +3% C2, -0.7% bunny.  BVH4 slab test with per-ray entry/exit plane selection (no min/max)
+// Per-translation-unit choices (the plain kernel's TU, rtx_capi.hip, takes the defaults; the
+// PARK TU, rtx_park.hip, sets its own before including this file).  Each was picked by A/B on
+// the scenes that run that TU's kernels (DESIGN.md ledger); every other alternative the
+// ledger records was measured and removed.
+#ifndef RTX_SINCOS_SMALL
+#define RTX_SINCOS_SMALL 1  // Lambertian cos/sin: 1 the restated small-argument forms, 0 the library's
 #endif
-#ifndef RTX_PHILOX_MAD
-#define RTX_PHILOX_MAD 1  // A/B r01: +2.3% C2, neutral bunny
+#ifndef RTX_TRI_BRANCHLESS
+#define RTX_TRI_BRANCHLESS 0  // kind-specialised walks: the triangle test without early exits
 #endif
-#ifndef RTX_PRIM_PRELOAD
-#define RTX_PRIM_PRELOAD 1  // primitive record in one batch of loads before the kind branch
+#ifndef RTX_EARLY_TEX
+#define RTX_EARLY_TEX 1  // textured builds: a Lambertian's albedo texture looked up before the sampling
 #endif
-#ifndef RTX_TAILHIST
-#define RTX_TAILHIST 0  // diagnostic build: histogram of active lanes per node-loop iteration
-#endif
-#ifndef RTX_NODE_LEAN
-#define RTX_NODE_LEAN 1  // BVH4 traversal without slot counts, slack folded into per-ray constants
-#endif
-#ifndef RTX_MERGED_SHADE
-#define RTX_MERGED_SHADE 1  // Sample() chains of the three materials in shared normalize/sqrt slots
-#endif
-#ifndef RTX_MAT_SOLID_INLINE
-#define RTX_MAT_SOLID_INLINE 1  // solid-colour textures resolved into the device material table
+#ifndef RTX_LEAF_STEP
+#define RTX_LEAF_STEP 0  // lean walk: at most one leaf test per lane and loop iteration (trace4_run_step)
 #endif
 
 namespace rtxd {
@@ -94,15 +89,10 @@ __device__ __forceinline__ void philox_block(uint32_t blk, uint32_t sample, uint
   uint32_t a = k0, b = k1;
 #pragma unroll
   for (int r = 0; r < 10; r++) {
-#if RTX_PHILOX_MAD
     // one v_mad_u64_u32 per product instead of v_mul_lo_u32 + v_mul_hi_u32
     const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
     uint32_t lo0 = (uint32_t)p0, hi0 = (uint32_t)(p0 >> 32);
     uint32_t lo1 = (uint32_t)p1, hi1 = (uint32_t)(p1 >> 32);
-#else
-    uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
-    uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
-#endif
     uint32_t n0 = hi1 ^ c1 ^ a;
     uint32_t n2 = hi0 ^ c3 ^ b;
     c0 = n0, c1 = lo1, c2 = n2, c3 = lo0;
@@ -167,13 +157,10 @@ __device__ __forceinline__ V3 random_in_unit_disk(Rng& g) {  // math_utils.h:83-
 // Lambertian angle 2*pi*r1 < 2*pi never takes, is not compiled in: its registers made the
 // shading spill.  -ffp-contract=off keeps every product and sum separately rounded, as in
 // the library; fma() is the library's fma.
-//   RTX_SINCOS_SMALL 0: the library's cos() and sin(); 1: both from one shared reduction;
-//   2: cos and sin each from its own small-argument reduction (fewest live registers: the
-//   plain kernel's texture-free builds lose their last spills, A/B r02 `ab_sincos2_*`).
+//   RTX_SINCOS_SMALL 1: cos and sin each from its own small-argument reduction (fewest live
+//   registers: the plain kernel's texture-free builds lose their last spills, A/B r02
+//   `ab_sincos2_*`; one shared reduction spilled more); 0: the library's cos() and sin().
 // Register allocation decides which is best per kernel, so the PARK TU picks its own value.
-#ifndef RTX_SINCOS_SMALL
-#define RTX_SINCOS_SMALL 2
-#endif
 __device__ __forceinline__ void sincos_small(double x, double& sn, double& cs) {
   // reduction: x = q * pi/2 + (hi + lo)
   const double q = rint(x * 0x1.45f306dc9c883p-1);
@@ -214,34 +201,15 @@ __device__ __forceinline__ void sincos_small(double x, double& sn, double& cs) {
   sn = quad > 1 ? -s0 : s0;
 }
 __device__ __forceinline__ void cos_sin(double phi, double& c, double& s) {
-#if RTX_SINCOS_SMALL == 2
+#if RTX_SINCOS_SMALL
   double t;
   sincos_small(phi, t, c);
   asm volatile("" : "+v"(c));
   asm volatile("" : "+v"(phi));
   sincos_small(phi, s, t);
-#elif RTX_SINCOS_SMALL
-  sincos_small(phi, s, c);
 #else
   c = cos(phi), s = sin(phi);
 #endif
-}
-
-__device__ __forceinline__ V3 random_cosine_direction(Rng& g, V3 normal) {  // math_utils.h:104-123
-  double r1 = g.next();
-  double r2 = g.next();
-  double phi = 2.0 * kPi * r1;
-  double r = sqrt(r2);
-  double cph, sph;
-  cos_sin(phi, cph, sph);
-  double x = r * cph;
-  double y = r * sph;
-  double z = sqrt(1.0 - r2);
-  V3 w = normalize(normal);
-  V3 a = (fabs(w.x) > 0.9) ? v3(0, 1, 0) : v3(1, 0, 0);
-  V3 v = normalize(cross(w, a));
-  V3 u = cross(v, w);
-  return normalize(x * u + y * v + z * w);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -252,24 +220,12 @@ struct DImage {
   const uint8_t* texels;
 };
 
-// Fast-path BVH2 node (RTX_PREC_FAST): both children's f32 boxes in the parent, so one
-// 64-byte line decides the near/far order.  Boxes are the f64 boxes rounded outward and
-// padded by the scene's conservative epsilon (see csrc/rtx_capi.hip build_fast_bvh).
-// child >= 0: internal node index; child < 0: leaf, ~child = first prim, count in cnt.
-struct FNode {
-  float lo0[3], hi0[3];
-  float lo1[3], hi1[3];
-  int32_t c0, c1;
-  uint16_t n0, n1;  // leaf primitive counts (0 for internal children)
-  uint32_t pad_;
-};
-static_assert(sizeof(FNode) == 64, "FNode must be one 64-byte line");
-
-// 4-wide fast node (RTX_PREC_FAST with RTX_BVH4): the reference's binary SAH tree collapsed
-// so every node holds up to four children's outward-rounded f32 boxes (SoA for the four
-// slab tests).  Leaves are the binary tree's leaves, unchanged.  child >= 0: node index;
-// child < 0: leaf, ~child = first prim, count in 16-bit half (c & 1) of counts[c >> 1];
-// empty slot: an empty leaf (child -1, count 0).  128 bytes = two cache lines.
+// 4-wide fast node (RTX_PREC_FAST): a binary SAH tree collapsed so every node holds up to four
+// children's outward-rounded f32 boxes (SoA for the four slab tests; build_fast4).  Every leaf
+// slot holds exactly one primitive: child >= 0: node index; child < 0: leaf, ~child = the
+// primitive; counts[]: 1 for a leaf slot (read by no kernel: the lean walk relies on the
+// one-primitive layout); an empty slot is an inverted box (lo = +inf, hi = -inf, child -1) that
+// no ray enters.  128 bytes = two cache lines.
 struct F4Node {
   float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4];  // axis a: lo at 32a, hi at 32a + 16 bytes
   int32_t child[4];
@@ -284,7 +240,6 @@ struct DScene {
   const rtx_material* mats;
   const rtx_texture* texs;
   const DImage* images;
-  const FNode* fnodes;  // fast layout (root at 0) or nullptr
   const F4Node* f4nodes;  // 4-wide fast layout (root at 0) or nullptr
   int64_t n_prims;
   int32_t use_bvh;
@@ -296,7 +251,7 @@ struct DScene {
   int32_t no_textures;     // no material reads the texture table (solid colours resolved at upload)
   int32_t n_global;   // fast BVH: primitives kept out of the tree, tested before every walk
   int32_t global[2];  // their indices into prims (see build_global_prims, rtx_capi.hip)
-  const double* tri_n;  // RTX_TRI_NORMALS: per primitive (x, y, z, 0), a triangle's unit normal, or nullptr
+  const double* tri_n;  // per primitive (x, y, z, 0), a triangle's unit normal (nullptr: no triangles)
 };
 
 struct Hit {  // HitRecord (hittable.h:18-42)
@@ -349,35 +304,11 @@ __device__ __forceinline__ bool hit_sphere(const double* g, int32_t mat, V3 o, V
   return true;
 }
 
-// Triangle edges e1 = B - A, e2 = C - A (triangle.h:45-46).  With RTX_TRI_EDGES the device
-// copy of the primitive table stores them in place of B and C (rtx_scene_create computes the
-// same IEEE double differences on the host), so the tests read them instead of subtracting.
-#ifndef RTX_TRI_EDGES
-#define RTX_TRI_EDGES 1
-#endif
-#ifndef RTX_TRI_NORMALS
-#define RTX_TRI_NORMALS 1  // a hit triangle's unit normal read from a table formed at upload (DScene::tri_n)
-#endif
-#ifndef RTX_TRI_BRANCHLESS
-#define RTX_TRI_BRANCHLESS 0  // traversal's triangle test without early exits (prim_t): 1 in kind-specialised tests, 2 in all; the PARK TU sets 1 (A/B r02: bunny +3.8 %, C5 plain kernel -1.9 %)
-#endif
-#ifndef RTX_EARLY_TEX
-#define RTX_EARLY_TEX 1  // textured builds: Lambertian albedo texture looked up before the sampling (shade_core; A/B r02: C5 +0.3 %)
-#endif
-#ifndef RTX_LAZY_RECT_UV
-#define RTX_LAZY_RECT_UV 1  // persistent shading: rect u,v derived from p at the image-texture lookup (like a sphere's)
-#endif
-#ifndef RTX_KIND_UNPINNED
-#define RTX_KIND_UNPINNED 1  // kind-specialised primitive tests do not load the kind word (A/B r02: bunny +0.3 %, C5 +0.3 %)
-#endif
-__device__ __forceinline__ V3 tri_e1(const double* g) {
-  if (RTX_TRI_EDGES) return V3{g[3], g[4], g[5]};
-  return V3{g[3], g[4], g[5]} - V3{g[0], g[1], g[2]};
-}
-__device__ __forceinline__ V3 tri_e2(const double* g) {
-  if (RTX_TRI_EDGES) return V3{g[6], g[7], g[8]};
-  return V3{g[6], g[7], g[8]} - V3{g[0], g[1], g[2]};
-}
+// Triangle edges e1 = B - A, e2 = C - A (triangle.h:45-46): the device copy of the primitive
+// table stores them in place of B and C (rtx_scene_create computes the same IEEE double
+// differences on the host), so the tests read them instead of subtracting.
+__device__ __forceinline__ V3 tri_e1(const double* g) { return V3{g[3], g[4], g[5]}; }
+__device__ __forceinline__ V3 tri_e2(const double* g) { return V3{g[6], g[7], g[8]}; }
 
 // Triangle::Hit (triangle.h:41-87): f32 det/inv_det/u/v/t, inclusive range, u,v untouched.
 __device__ __forceinline__ bool hit_triangle(const double* g, int32_t mat, V3 o, V3 d, double tmin, double tmax,
@@ -464,14 +395,13 @@ struct PrimRec {
 template <bool KIND_KNOWN = false>
 __device__ __forceinline__ PrimRec load_prim(const rtx_prim* __restrict__ P, bool tris) {
   PrimRec r;
-#if RTX_PRIM_PRELOAD
   // spheres and rects read g[0..4] (48 bytes); triangles g[0..8] (80 bytes)
   const uint4 w0 = *(const uint4*)P;
   const double2 w1 = *((const double2*)P + 1), w2 = *((const double2*)P + 2);
   double2 w3 = make_double2(0.0, 0.0), w4 = make_double2(0.0, 0.0);
   if (tris) w3 = *((const double2*)P + 3), w4 = *((const double2*)P + 4);
   // (a kind-specialised caller never reads the kind word: it is not pinned, so not loaded)
-  if (!(RTX_KIND_UNPINNED && KIND_KNOWN)) asm volatile("" ::"v"(w0.x));
+  if (!KIND_KNOWN) asm volatile("" ::"v"(w0.x));
   asm volatile("" ::"v"(w0.z), "v"(w0.w), "v"(w1.x), "v"(w1.y), "v"(w2.x), "v"(w2.y), "v"(w3.x), "v"(w3.y),
                "v"(w4.x), "v"(w4.y));
   r.kind = (int)w0.x;
@@ -479,12 +409,6 @@ __device__ __forceinline__ PrimRec load_prim(const rtx_prim* __restrict__ P, boo
   r.g[0] = __hiloint2double((int)w0.w, (int)w0.z);
   r.g[1] = w1.x, r.g[2] = w1.y, r.g[3] = w2.x, r.g[4] = w2.y;
   r.g[5] = w3.x, r.g[6] = w3.y, r.g[7] = w4.x, r.g[8] = w4.y;
-#else
-  r.kind = P->kind;
-  r.mat = P->material;
-#pragma unroll
-  for (int i = 0; i < 9; i++) r.g[i] = P->g[i];
-#endif
   return r;
 }
 
@@ -509,7 +433,7 @@ __device__ __forceinline__ bool prim_t_rec(const PrimRec& R, V3 o, V3 d, double 
   mat_out = R.mat;
   const PrimRec* P = &R;
   const int kind = KIND >= 0 ? KIND : P->kind;
-  if (RTX_TRI_BRANCHLESS && (RTX_TRI_BRANCHLESS == 2 || KIND >= 0) && kind == RTX_PRIM_TRIANGLE) {
+  if (RTX_TRI_BRANCHLESS && KIND >= 0 && kind == RTX_PRIM_TRIANGLE) {
     // the same operations without the early exits: every value is computed and the four
     // rejections are combined at the end (a wave's few active leaf lanes rarely all take
     // the same early exit, so the branches only add mask bookkeeping)
@@ -613,7 +537,7 @@ __device__ __forceinline__ void finish_hit_at(const DScene& S, int64_t best, dou
     else h.lazy_uv = best;
   } else if (kind == RTX_PRIM_TRIANGLE) {  // hit_triangle after t
     h.p = o + h.t * d;
-    if (RTX_TRI_NORMALS && S.tri_n) {
+    if (S.tri_n) {
       // normalize(cross(B - A, C - A)) formed at upload in the same IEEE double operations
       const double2 n01 = *(const double2*)(S.tri_n + 4 * best), n2 = *(const double2*)(S.tri_n + 4 * best + 2);
       set_face_normal(h, d, V3{n01.x, n01.y, n2.x});
@@ -627,7 +551,7 @@ __device__ __forceinline__ void finish_hit_at(const DScene& S, int64_t best, dou
     if (kind == RTX_PRIM_XY_RECT) a0 = 0, a1 = 1, n = v3(0, 0, 1);
     else if (kind == RTX_PRIM_XZ_RECT) a0 = 0, a1 = 2, n = v3(0, 1, 0);
     else a0 = 1, a1 = 2, n = v3(1, 0, 0);
-    if (UV || !RTX_LAZY_RECT_UV) {
+    if (UV) {
       const double x = comp(o, a0) + t * comp(d, a0);
       const double y = comp(o, a1) + t * comp(d, a1);
       h.u = (x - P->g[0]) / (P->g[1] - P->g[0]);
@@ -664,11 +588,6 @@ struct Counters {
   uint32_t nodes, prims;  // lane-level node visits / primitive tests
   uint32_t wnodes, wprims;  // wave-level loop iterations (counted by the first active lane)
   uint32_t tris, sphs;      // primitive tests by kind (rects = prims - tris - sphs)
-#if RTX_TAILHIST
-  uint32_t tail[6];  // diagnostic: node-loop wave iterations with <= 1, 2, 4, 8, 16, 32 active lanes
-  uint32_t leafph[4];  // diagnostic: node iterations whose leaf loop runs 1..4 wave iterations
-  uint32_t leaft;      //   and the leaf tests those iterations hold (lane level)
-#endif
 };
 __device__ __forceinline__ void count_prim(Counters& c, const rtx_prim* P) {
   c.prims++;
@@ -732,110 +651,14 @@ __device__ __forceinline__ int64_t trace_parity(const DScene& S, V3 o, V3 d, dou
 // nearer child first; leaves are tested with the exact f64 primitive routines above.
 // Enlarged boxes accept every ray the f64 test accepts, so the set of primitives that can
 // produce the closest hit is a superset of the reference's; the closest hit is the same
-// except for exact-tie orderings between distinct primitives (measure zero).
+// except for exact-tie orderings between distinct primitives (tests/test_gpu_parity.py checks
+// every differing record is such a tie).
 // ---------------------------------------------------------------------------------------
-// The f64 origin is split into hi + lo floats so that (box - origin) is formed with a
-// RELATIVE rounding error (no absolute error from rounding |o| to f32); together with the
-// relative slack below and outward-rounded boxes the f32 test never rejects a box the
-// reference's f64 test accepts.
-struct FRay {
-  float ohx, ohy, ohz, olx, oly, olz, ix, iy, iz;
-};
-__device__ __forceinline__ FRay make_fray(V3 o, V3 d) {
-  FRay r;
-  r.ohx = (float)o.x, r.ohy = (float)o.y, r.ohz = (float)o.z;
-  r.olx = (float)(o.x - (double)r.ohx), r.oly = (float)(o.y - (double)r.ohy), r.olz = (float)(o.z - (double)r.ohz);
-  r.ix = 1.0f / (float)d.x, r.iy = 1.0f / (float)d.y, r.iz = 1.0f / (float)d.z;
-  return r;
-}
-// Returns the (slack-widened) entry distance, or +inf on a miss.
-__device__ __forceinline__ float fbox(const float* lo, const float* hi, const FRay& r, float tmin_f, float tmax_f) {
-  float tx0 = ((lo[0] - r.ohx) - r.olx) * r.ix, tx1 = ((hi[0] - r.ohx) - r.olx) * r.ix;
-  float ty0 = ((lo[1] - r.ohy) - r.oly) * r.iy, ty1 = ((hi[1] - r.ohy) - r.oly) * r.iy;
-  float tz0 = ((lo[2] - r.ohz) - r.olz) * r.iz, tz1 = ((hi[2] - r.ohz) - r.olz) * r.iz;
-  // fminf/fmaxf drop a NaN operand (0*inf for an axis-parallel ray on a slab plane); the
-  // reference rejects those rays, so dropping the constraint only widens the accepted set.
-  float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), tmin_f));
-  float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax_f));
-  tn = tn * 0.99999f;  // relative slack >> the ~6 ulp of f32 rounding in the products
-  tf = tf * 1.00001f;
-  return tn <= tf ? tn : __builtin_inff();
-}
-
 // smallest float >= x (x > 0 or +inf here)
 __device__ __forceinline__ float f32_round_up(double x) {
   float f = (float)x;
   if ((double)f < x) f = __int_as_float(__float_as_int(f) + (f >= 0.0f ? 1 : -1));
   return f;
-}
-
-template <int STACK, bool COUNT>
-__device__ __forceinline__ int64_t trace_fast(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
-                                              int stride, Counters& cnt, double& t_best) {
-  int64_t best = -1;
-  double closest = tmax, t;
-  if (!S.use_bvh || S.froot_leaf) {
-    const int64_t n = S.use_bvh ? S.froot_count : S.n_prims;
-    for (int64_t i = 0; i < n; i++) {
-      if (COUNT) count_prim(cnt, S.prims + i);
-      if (prim_t(S.prims + i, S.has_tris, o, d, tmin, closest, t)) closest = t, best = i;
-    }
-    t_best = closest;
-    return best;
-  }
-  const FRay r = make_fray(o, d);
-  const float tmin_f = 0.0f;  // boxes only need t >= 0 for conservativeness (tmin > 0)
-  float tmax_f = f32_round_up(closest);
-  int sp = 0;
-  int32_t node = 0;
-  while (true) {
-    const FNode* __restrict__ nd = S.fnodes + node;
-    float lo0[3] = {nd->lo0[0], nd->lo0[1], nd->lo0[2]}, hi0[3] = {nd->hi0[0], nd->hi0[1], nd->hi0[2]};
-    float lo1[3] = {nd->lo1[0], nd->lo1[1], nd->lo1[2]}, hi1[3] = {nd->hi1[0], nd->hi1[1], nd->hi1[2]};
-    int32_t c0 = nd->c0, c1 = nd->c1;
-    uint32_t n0 = nd->n0, n1 = nd->n1;
-    if (COUNT) cnt.nodes++;
-    float t0 = fbox(lo0, hi0, r, tmin_f, tmax_f);
-    float t1 = fbox(lo1, hi1, r, tmin_f, tmax_f);
-    bool h0 = t0 != __builtin_inff(), h1 = t1 != __builtin_inff();
-    // leaves are processed immediately, internal children are traversed near-first
-    bool shrink = false;
-    if (h0 && c0 < 0) {
-      uint32_t first = (uint32_t)(~c0);
-      for (uint32_t i = 0; i < n0; i++) {
-        if (COUNT) count_prim(cnt, S.prims + first + i);
-        if (prim_t(S.prims + first + i, S.has_tris, o, d, tmin, closest, t)) closest = t, best = (int64_t)first + i, shrink = true;
-      }
-      h0 = false;
-    }
-    if (h1 && c1 < 0) {
-      uint32_t first = (uint32_t)(~c1);
-      for (uint32_t i = 0; i < n1; i++) {
-        if (COUNT) count_prim(cnt, S.prims + first + i);
-        if (prim_t(S.prims + first + i, S.has_tris, o, d, tmin, closest, t)) closest = t, best = (int64_t)first + i, shrink = true;
-      }
-      h1 = false;
-    }
-    if (shrink) tmax_f = f32_round_up(closest);
-    if (h0 && h1) {
-      int32_t nearc = t0 <= t1 ? c0 : c1;
-      int32_t farc = t0 <= t1 ? c1 : c0;
-      if (sp + 1 > STACK) __builtin_trap();
-      stk[(sp++) * stride] = (uint32_t)farc;
-      node = nearc;
-    } else if (h0) {
-      node = c0;
-    } else if (h1) {
-      node = c1;
-    } else {
-      // pop, re-testing the popped node's box against the shrunk interval is implicit:
-      // its box was tested when pushed; a stale far child is re-culled at its own node.
-      if (sp == 0) break;
-      node = (int32_t)stk[(--sp) * stride];
-    }
-  }
-  t_best = closest;
-  return best;
 }
 
 // Pins a value at this point of the program (no code): the compiler can neither move its
@@ -853,53 +676,28 @@ __device__ __forceinline__ void pin(V3& v) {
 // carries the outward-rounded box of the binary node it replaces, and the slab test below is
 // conservative), so the candidate primitive set contains the reference's and the closest
 // hit is the same up to exact t ties.  Per node: four slab tests, the hit leaves' primitives
-// in one flattened loop (lanes stay converged whichever slots they hit), then the surviving
-// internal children sorted by entry distance; the nearest is visited next, the others are
-// pushed far-to-near.  The host sizes STACK from the exact worst-case push depth of the
-// collapsed tree (rtx_capi.hip build_fast4).
+// (one per leaf slot), then the surviving internal children sorted by entry distance; the
+// nearest is visited next, the others are pushed far-to-near.  The host sizes the stack from
+// the exact worst-case push depth of the collapsed tree (rtx_capi.hip build_fast4).
 //
 // Slab test, one FMA per plane: t = fma(plane, inv, n) with n = -(o * inv) -/+ delta.
-// With inv = 1/RN(d) to within one ulp (v_rcp_f32, RTX_SLAB_RCP; or RN(1/RN(d)), the IEEE
-// division), o_f = RN(o), n0 = RN(-o_f * inv), the computed plane distance is
+// With inv = 1/RN(d) to within one ulp (v_rcp_f32), o_f = RN(o), n0 = RN(-o_f * inv), the
+// computed plane distance is
 //   t_c = T (1 + e_rel) + E,  |e_rel| <= 2^-22 + 2^-24,  |E| <= |o * inv| * 2^-23 * (1 + 2^-20)
 // against the exact T = (plane - o) / d.  E is absorbed by shifting n outward by
 // delta = |n0| * 2^-20 (the entry plane's offset down, the exit plane's up, by the sign of
 // inv), e_rel by the 1e-5 relative slack on the entry/exit distances.  An axis whose offset
 // is not finite (inv = inf for a zero f32 component) is neutralised: inv = 0, n = -/+inf,
 // i.e. the slab imposes no constraint — a widening, hence still conservative.
-struct FRay4 {
-  float ix, iy, iz, nlx, nhx, nly, nhy, nlz, nhz;
-#if RTX_SIGNED_PLANES
-  uint32_t ox, oy, oz;  // byte offset of the entry-plane array per axis (exit plane: offset ^ 16)
-#endif
-};
-#ifndef RTX_SLAB_RCP
-#define RTX_SLAB_RCP 1  // slab inverses by the hardware reciprocal (1 ulp) instead of the IEEE division sequence
-#endif
-__device__ __forceinline__ float slab_inv(float d) {
-  // a zero or denormal d gives +-inf or a huge inverse either way; the caller neutralises an
-  // axis whose offset is not finite
-  return RTX_SLAB_RCP ? __builtin_amdgcn_rcpf(d) : 1.0f / d;
-}
-__device__ __forceinline__ void fray4_axis(double o, double d, float& inv, float& nl, float& nh) {
-  inv = slab_inv((float)d);
-  const float n0 = -((float)o * inv);
-  if (!(fabsf(n0) < __builtin_inff())) {
-    inv = 0.0f, nl = -__builtin_inff(), nh = __builtin_inff();
-    return;
-  }
-  const float delta = fabsf(n0) * 0x1p-20f;
-  // plane `lo` enters when inv >= 0 (offset down), exits when inv < 0 (offset up)
-  nl = inv >= 0.0f ? n0 - delta : n0 + delta;
-  nh = inv >= 0.0f ? n0 + delta : n0 - delta;
-}
-#if RTX_SIGNED_PLANES
+//
 // Sign-selected planes: the entry plane of axis a is `lo` when inv >= 0 and `hi` otherwise,
 // so each slab needs no min/max: nl is the entry offset (n0 - delta), nh the exit offset
 // (n0 + delta), and the entry-plane array is picked by a per-ray byte offset into the node.
 __device__ __forceinline__ void fray4_axis_signed(double o, double d, int axis, float& inv, float& nl, float& nh,
                                                   uint32_t& off) {
-  inv = slab_inv((float)d);
+  // the hardware reciprocal (1 ulp; a zero or denormal d gives +-inf or a huge inverse, and
+  // an axis whose offset is not finite is neutralised below)
+  inv = __builtin_amdgcn_rcpf((float)d);
   const float n0 = -((float)o * inv);
   off = 32u * axis;
   if (!(fabsf(n0) < __builtin_inff())) {
@@ -910,43 +708,7 @@ __device__ __forceinline__ void fray4_axis_signed(double o, double d, int axis, 
   nl = n0 - delta, nh = n0 + delta;
   if (inv < 0.0f) off += 16u;
 }
-#endif
-__device__ __forceinline__ FRay4 make_fray4(V3 o, V3 d) {
-  FRay4 r;
-#if RTX_SIGNED_PLANES
-  fray4_axis_signed(o.x, d.x, 0, r.ix, r.nlx, r.nhx, r.ox);
-  fray4_axis_signed(o.y, d.y, 1, r.iy, r.nly, r.nhy, r.oy);
-  fray4_axis_signed(o.z, d.z, 2, r.iz, r.nlz, r.nhz, r.oz);
-#else
-  fray4_axis(o.x, d.x, r.ix, r.nlx, r.nhx);
-  fray4_axis(o.y, d.y, r.iy, r.nly, r.nhy);
-  fray4_axis(o.z, d.z, r.iz, r.nlz, r.nhz);
-#endif
-  return r;
-}
 __device__ __forceinline__ float f4c(const float4& v, int c) { return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w)); }
-// slab test from entry/exit plane values (sign-selected): entry distance or +inf
-__device__ __forceinline__ float fbox4s(float ex, float ey, float ez, float fx, float fy, float fz, const FRay4& r,
-                                        float tmax_f) {
-  float tn = fmaxf(fmaxf(fmaf(ex, r.ix, r.nlx), fmaf(ey, r.iy, r.nly)), fmaxf(fmaf(ez, r.iz, r.nlz), 0.0f));
-  float tf = fminf(fminf(fmaf(fx, r.ix, r.nhx), fmaf(fy, r.iy, r.nhy)), fminf(fmaf(fz, r.iz, r.nhz), tmax_f));
-  tn = tn * 0.99999f;
-  tf = tf * 1.00001f;
-  return tn <= tf ? tn : __builtin_inff();
-}
-// entry distance (slack-widened) or +inf on a miss; NaN plane distances drop out of the
-// min/max (v_min/v_max_f32 return the non-NaN operand), which only widens the interval
-__device__ __forceinline__ float fbox4(float lx, float ly, float lz, float hx, float hy, float hz, const FRay4& r,
-                                       float tmax_f) {
-  const float tx0 = fmaf(lx, r.ix, r.nlx), tx1 = fmaf(hx, r.ix, r.nhx);
-  const float ty0 = fmaf(ly, r.iy, r.nly), ty1 = fmaf(hy, r.iy, r.nhy);
-  const float tz0 = fmaf(lz, r.iz, r.nlz), tz1 = fmaf(hz, r.iz, r.nhz);
-  float tn = fmaxf(fmaxf(fminf(tx0, tx1), fminf(ty0, ty1)), fmaxf(fminf(tz0, tz1), 0.0f));
-  float tf = fminf(fminf(fmaxf(tx0, tx1), fmaxf(ty0, ty1)), fminf(fmaxf(tz0, tz1), tmax_f));
-  tn = tn * 0.99999f;  // tn >= 0
-  tf = tf * 1.00001f;  // only tf >= tn >= 0 can pass
-  return tn <= tf ? tn : __builtin_inff();
-}
 
 __device__ __forceinline__ void cswap4(float& ta, int32_t& ca, float& tb, int32_t& cb) {
   const bool s = tb < ta;
@@ -958,136 +720,23 @@ __device__ __forceinline__ void cswap4(float& ta, int32_t& ca, float& tb, int32_
   ca = c;
 }
 
-template <int STACK, bool COUNT>
-__device__ __forceinline__ int64_t trace_fast4(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
-                                               int stride, Counters& cnt, double& t_best, int32_t& mat_best) {
-  int64_t best = -1;
-  double closest = tmax, t;
-  int32_t m;
-  mat_best = -1;
-  if (!S.use_bvh || S.froot_leaf) {
-    const int64_t n = S.use_bvh ? S.froot_count : S.n_prims;
-    for (int64_t i = 0; i < n; i++) {
-      if (COUNT) count_prim(cnt, S.prims + i);
-      if (prim_t(S.prims + i, S.has_tris, o, d, tmin, closest, t, m)) closest = t, best = i, mat_best = m;
-    }
-    t_best = closest;
-    return best;
-  }
-  for (int i = 0; i < S.n_global; i++) {
-    const int64_t gi = S.global[i];
-    if (COUNT) count_prim(cnt, S.prims + gi);
-    if (prim_t(S.prims + gi, S.has_tris, o, d, tmin, closest, t, m)) closest = t, best = gi, mat_best = m;
-  }
-  const FRay4 r = make_fray4(o, d);
-  float tmax_f = f32_round_up(closest);
-  int sp = 0;
-  int32_t node = 0;
-  while (true) {
-    const F4Node* __restrict__ nd = S.f4nodes + node;
-    if (COUNT) {
-      cnt.nodes++;
-      if (first_active_lane()) cnt.wnodes++;
-    }
-    float tt[4];
-    int32_t cc[4];
-    const uint32_t counts01 = nd->counts[0], counts23 = nd->counts[1];
-#if RTX_SIGNED_PLANES
-    {
-      const char* nb = (const char*)nd;
-      const float4 ex = *(const float4*)(nb + r.ox), fx = *(const float4*)(nb + (r.ox ^ 16u));
-      const float4 ey = *(const float4*)(nb + r.oy), fy = *(const float4*)(nb + (r.oy ^ 16u));
-      const float4 ez = *(const float4*)(nb + r.oz), fz = *(const float4*)(nb + (r.oz ^ 16u));
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        tt[c] = fbox4s(f4c(ex, c), f4c(ey, c), f4c(ez, c), f4c(fx, c), f4c(fy, c), f4c(fz, c), r, tmax_f);
-        cc[c] = nd->child[c];
-      }
-    }
-#else
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      tt[c] = fbox4(nd->lox[c], nd->loy[c], nd->loz[c], nd->hix[c], nd->hiy[c], nd->hiz[c], r, tmax_f);
-      cc[c] = nd->child[c];
-    }
-#endif
-    // hit leaves (non-empty) -> mask; they leave the internal-child ordering
-    uint32_t lmask = 0;
-#pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const uint32_t n = ((c < 2 ? counts01 : counts23) >> (16 * (c & 1))) & 0xffffu;
-      if (cc[c] < 0) {
-        if (tt[c] != __builtin_inff() && n != 0) lmask |= 1u << c;
-        tt[c] = __builtin_inff();
-      }
-    }
-    if (lmask) {
-      bool shrink = false;
-      uint32_t cur = 0, left = 0;
-      while (lmask | left) {
-        if (left == 0) {
-          const int c = __builtin_ctz(lmask);
-          lmask &= lmask - 1u;
-          // two-level select (v_cndmask) rather than a compare chain the compiler branches on
-          const int32_t c01 = (c & 1) ? cc[1] : cc[0], c23 = (c & 1) ? cc[3] : cc[2];
-          cur = (uint32_t)(~((c & 2) ? c23 : c01));
-          left = (((c & 2) ? counts23 : counts01) >> (16 * (c & 1))) & 0xffffu;
-        }
-        if (COUNT) {
-          count_prim(cnt, S.prims + cur);
-          if (first_active_lane()) cnt.wprims++;
-        }
-        if (prim_t(S.prims + cur, S.has_tris, o, d, tmin, closest, t, m))
-          closest = t, best = (int64_t)cur, mat_best = m, shrink = true;
-        cur++, left--;
-      }
-      if (shrink) {
-        tmax_f = f32_round_up(closest);
-#pragma unroll
-        for (int c = 0; c < 4; c++)
-          if (tt[c] > tmax_f) tt[c] = __builtin_inff();
-      }
-    }
-    cswap4(tt[0], cc[0], tt[1], cc[1]);
-    cswap4(tt[2], cc[2], tt[3], cc[3]);
-    cswap4(tt[0], cc[0], tt[2], cc[2]);
-    cswap4(tt[1], cc[1], tt[3], cc[3]);
-    cswap4(tt[1], cc[1], tt[2], cc[2]);
-    if (tt[0] != __builtin_inff()) {
-#pragma unroll
-      for (int c = 3; c >= 1; c--) {
-        if (tt[c] != __builtin_inff()) {
-          if (sp + 1 > STACK) __builtin_trap();
-          stk[(sp++) * stride] = (uint32_t)cc[c];
-        }
-      }
-      node = cc[0];
-    } else {
-      if (sp == 0) break;
-      node = (int32_t)stk[(--sp) * stride];
-    }
-  }
-  t_best = closest;
-  return best;
-}
-
-// Lean variant of trace_fast4 (RTX_NODE_LEAN, default).  Relies on build_fast4's layout
-// guarantees: every leaf slot holds exactly one primitive and empty slots have an inverted
-// box, so the per-slot counts are not read.  The 1e-5 relative slack of the slab test is
-// folded into per-ray constants instead of two multiplies per slot:
+// The 1e-5 relative slack of the slab test is folded into per-ray constants instead of two
+// multiplies per slot:
 //   tn' = fma(plane, inv * (1 - s), nl * (1 - s)),  tf' = fma(plane, inv * (1 + s), nh * (1 + s))
 // i.e. (1 -/+ s) times each plane distance (monotone, so it commutes with the min/max and
 // with the clamp at 0); the extra rounding of the two products is < 2^-23 relative, far
-// inside s = 1e-5, and < 2^-23 |n0| absolute, inside the outward offset delta = 2^-20 |n0|
-// (see FRay4), so the test stays conservative.  Node loads use a 32-bit byte offset from the
-// (uniform) node-array base.
-#ifndef RTX_PUSH_BRANCHLESS
-#define RTX_PUSH_BRANCHLESS 1  // lean walk: unconditional child stores, sp advanced per entered child
-#endif
+// inside s = 1e-5, and < 2^-23 |n0| absolute, inside the outward offset delta = 2^-20 |n0|,
+// so the test stays conservative.  The walk relies on build_fast4's layout guarantees: every
+// leaf slot holds exactly one primitive and empty slots have an inverted box, so no per-slot
+// count is read.  Node loads use a 32-bit byte offset from the (uniform) node-array base.
 struct FRay4L {
   float iex, iey, iez, nex, ney, nez;  // entry planes: inverse and offset, scaled by (1 - s)
   float ixx, ixy, ixz, nxx, nxy, nxz;  // exit planes: scaled by (1 + s)
   uint32_t ox, oy, oz;                 // byte offset of the entry-plane array per axis (exit: ^ 16)
+};
+struct FRay4 {  // per-ray plane constants before the slack is folded in
+  float ix, iy, iz, nlx, nhx, nly, nhy, nlz, nhz;
+  uint32_t ox, oy, oz;  // byte offset of the entry-plane array per axis (exit plane: offset ^ 16)
 };
 __device__ __forceinline__ FRay4L make_fray4l(V3 o, V3 d) {
   FRay4 b;
@@ -1176,7 +825,7 @@ __device__ __forceinline__ uint32_t leaf_prim(const int32_t (&cc)[4], int c) {
 }
 // The end of a visit: after a new closest hit (shrink), the children entered beyond it are
 // dropped; the rest are sorted near to far, the nearest is visited next and the others pushed
-// (branchless, RTX_PUSH_BRANCHLESS: the sort leaves the entered children as a prefix, so the
+// (branchless: the sort leaves the entered children as a prefix, so the
 // stores at sp are unconditional and sp advances per entered child; build_fast4 bounds sp by
 // the tree's exact worst case, and the kernels give each lane STACK + 1 slots), or the stack
 // is popped.  false: the stack was empty, the walk is over.
@@ -1197,21 +846,11 @@ __device__ __forceinline__ bool visit_next(float (&tt)[4], int32_t (&cc)[4], boo
   cswap4(tt[1], cc[1], tt[3], cc[3]);
   cswap4(tt[1], cc[1], tt[2], cc[2]);
   if (tt[0] != __builtin_inff()) {
-#if RTX_PUSH_BRANCHLESS
 #pragma unroll
     for (int c = 3; c >= 1; c--) {
       stk[sp * stride] = (SE)cc[c];
       sp += tt[c] != __builtin_inff() ? 1 : 0;
     }
-#else
-#pragma unroll
-    for (int c = 3; c >= 1; c--) {
-      if (tt[c] != __builtin_inff()) {
-        if (sp + 1 > STACK) __builtin_trap();
-        stk[(sp++) * stride] = (uint32_t)cc[c];
-      }
-    }
-#endif
     node = (uint32_t)cc[0];
     return true;
   }
@@ -1220,11 +859,6 @@ __device__ __forceinline__ bool visit_next(float (&tt)[4], int32_t (&cc)[4], boo
   return true;
 }
 
-#ifndef RTX_LEAF_STEP
-// lean walk: at most one leaf test per lane and loop iteration (trace4_run_step); the PARK TU
-// sets 1 (A/B r02: bunny +2.8 %, C2 -1.5 %, C5 -1.9 %)
-#define RTX_LEAF_STEP 0
-#endif
 // The lean walk with its leaf tests spread over loop iterations.  A node visit whose boxes
 // admit L leaf slots keeps the lane on that node for max(1, L) iterations: the slab tests and
 // the first leaf test in the first, one more leaf test in each further one, and the stack
@@ -1397,24 +1031,10 @@ __device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double t
     if (COUNT) {
       cnt.nodes++;
       if (first_active_lane()) cnt.wnodes++;
-#if RTX_TAILHIST
-      const int act = __popcll(__ballot(1));
-      if (first_active_lane())
-        for (int i = 0; i < 6; i++) cnt.tail[i] += act <= (1 << i) ? 1u : 0u;
-#endif
     }
     float tt[4];
     int32_t cc[4];
     uint32_t lmask = visit_slabs(nbase, node, r, tmax_x, tt, cc);
-#if RTX_TAILHIST
-    if (COUNT) {
-      const int nl = __popc(lmask);
-      int mx = 0;
-      for (int k = 1; k <= 4; k++) mx = __ballot(nl >= k) ? k : mx;
-      if (first_active_lane() && mx > 0) cnt.leafph[mx - 1]++;
-      cnt.leaft += nl;
-    }
-#endif
     if (lmask) {
       bool shrink = false;
       while (lmask) {  // the visit's leaf slots, in slot order
@@ -1482,16 +1102,9 @@ __device__ __forceinline__ int64_t trace_fast4_lean(const DScene& S, V3 o, V3 d,
 // as hit_sphere; a rect's (x - x0) / (x1 - x0), (y - y0) / (y1 - y0) (rect.h), where x and y
 // are p's in-plane components (hit_rect's x = o + t d per component, the same operations as
 // p = o + t d).
-// (Returned by value: reference outputs of a call live in scratch memory.)
-#ifndef RTX_LAZY_UV_INLINE
-#define RTX_LAZY_UV_INLINE 0  // 1: inlined instead of called
-#endif
-#if RTX_LAZY_UV_INLINE
-__device__ __forceinline__
-#else
-__device__ __noinline__
-#endif
-double2 lazy_uv(const rtx_prim* __restrict__ P, V3 p) {
+// (Returned by value: reference outputs of a call live in scratch memory.  A call, not
+// inlined: inlined, the textured build spills 300 B per lane, ledger.)
+__device__ __noinline__ double2 lazy_uv(const rtx_prim* __restrict__ P, V3 p) {
   double2 uv;
   const int kind = P->kind;
   if (kind == RTX_PRIM_SPHERE) {
@@ -1563,60 +1176,6 @@ __device__ __forceinline__ double reflectance(double c, double ri) {  // materia
   double r0 = (1.0 - ri) / (1.0 + ri);
   r0 = r0 * r0;
   return r0 + (1.0 - r0) * pow5(1.0 - c);
-}
-
-// Material::Sample (material.cc:57-74, 117-141, 194-256, 302-310)
-__device__ __forceinline__ bool mat_sample(const DScene& S, const rtx_material& m, const Hit& rec, V3 wo, V3& wi,
-                                           float& pdf, V3& f, Rng& g) {
-  if (m.kind == RTX_MAT_LAMBERTIAN) {
-    wi = random_cosine_direction(g, rec.normal);
-    if (dot(wi, rec.normal) <= 0) return false;
-    float c = (float)dot(rec.normal, wi);
-    pdf = (c <= 0.0f) ? 0.0f : (float)((double)c / kPi);
-    if (dot(rec.normal, wi) <= 0) f = v3(0, 0, 0);
-    else f = mat_tex(S, m, rec) / kPi;
-    return true;
-  }
-  if (m.kind == RTX_MAT_METAL) {
-    wi = reflect(-wo, rec.normal);
-    wi = wi + m.fuzz * random_unit_vector(g);
-    wi = normalize(wi);
-    if (dot(wi, rec.normal) <= 0) return false;
-    pdf = 1.0f;
-    f = v3(m.albedo[0], m.albedo[1], m.albedo[2]);
-    return true;
-  }
-  if (m.kind == RTX_MAT_DIELECTRIC) {
-    V3 n = rec.normal;
-    double eta_i = 1.0, eta_t = m.ref_idx;
-    if (!rec.front_face) {
-      double tt = eta_i;
-      eta_i = eta_t, eta_t = tt;
-    }
-    double eta = eta_i / eta_t;
-    V3 win = -normalize(wo);
-    double ci = dot(win, n);
-    ci = ci < -1.0 ? -1.0 : (ci > 1.0 ? 1.0 : ci);
-    double si = sqrt(fmax(0.0, 1.0 - ci * ci));
-    double st = eta * si;
-    pdf = 1.0f;
-    if (st >= 1.0) {
-      wi = reflect(win, n);
-      f = v3(1.0, 1.0, 1.0);
-      return true;
-    }
-    double Fr = reflectance(fabs(ci), m.ref_idx);
-    if (g.next() < Fr) {
-      wi = reflect(win, n);
-      f = v3(1.0, 1.0, 1.0);
-      return true;
-    }
-    wi = refract(win, n, eta);
-    double k = eta * eta;
-    f = v3(k, k, k);
-    return true;
-  }
-  return false;  // DiffuseLight
 }
 
 // Material::Scatter (material.cc:20-34, 82-94, 148-172, 273-280) — megakernel mode
@@ -1719,7 +1278,10 @@ __device__ __forceinline__ V3 normalize_l(V3 v, double& l) {
 // in five shared slots: a wave that holds lanes of several materials executes each
 // normalize / sqrt once for all of them, instead of once per material branch.  Every lane
 // still performs exactly its own material's operations on its own operands, in the
-// reference's order, so the results are bit-identical to shade_by_material below:
+// reference's order, so the results are bit-identical to one branch per material (the
+// Lambertian chain is math_utils.h:104-123 RandomCosineDirection; the merge was checked bit
+// for bit against the per-material form, cmp_merged_shade_bitexact.txt, before that form was
+// removed):
 //   slot 1 normalize   Lambertian: w = normalize(n)          Dielectric: win = normalize(d)
 //   slot 2 sqrt        Lambertian: sqrt(r2)                  Dielectric: sqrt(max(0, 1 - ci^2))
 //   slot 3 sqrt        Lambertian: sqrt(1 - r2)              Dielectric (refract): sqrt|1 - |perp|^2|
@@ -1923,52 +1485,10 @@ __device__ __forceinline__ bool shade_merged(const DScene& S, int max_depth, Pat
   return shade_finish(so, p.thr, p.depth, g, L);
 }
 
-// The same step with one Sample() branch per material (mat_sample): the reference's
-// structure, kept for the A/B build (RTX_MERGED_SHADE=0) and as the readable statement.
-__device__ __forceinline__ bool shade_by_material(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit,
-                                                  Rng& g, V3& L, const rtx_material& m) {
-  L = v3(0, 0, 0);
-  if (!hit || p.depth >= max_depth) {
-    L = L + p.thr * sky(p.d);
-    return false;
-  }
-  V3 em = mat_emitted(S, m, rec);
-  if (!near_zero(em)) {
-    L = L + p.thr * em;
-    return false;
-  }
-  V3 wo = -normalize(p.d);
-  V3 wi, f;
-  float pdf = 0.0f;
-  if (!mat_sample(S, m, rec, wo, wi, pdf, f, g)) return false;
-  Path c;
-  c.o = rec.p, c.d = wi, c.depth = p.depth + 1;
-  if (m.kind != RTX_MAT_LAMBERTIAN) {  // IsSpecular
-    c.thr = p.thr * f;
-  } else {
-    if (pdf < 1e-6f) return false;
-    float ct = fmaxf(0.0f, (float)dot(wi, rec.normal));
-    c.thr = ((double)ct * (p.thr * f)) / (double)pdf;
-  }
-  if (c.depth > 5) {  // Russian roulette (wavefront.cc:189-205)
-    double q = fmax(fmax(c.thr.x, c.thr.y), c.thr.z);
-    q = q < 0.1 ? 0.1 : (q > 0.95 ? 0.95 : q);
-    if (g.next() > q) return false;
-    c.thr = c.thr / q;
-  }
-  p = c;
-  return true;
-}
-
-
 template <bool LAMB = false, bool NOTEX = false>
 __device__ __forceinline__ bool shade(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit, Rng& g,
                                       V3& L, const rtx_material& m) {
-#if RTX_MERGED_SHADE
   return shade_merged<LAMB, NOTEX>(S, max_depth, p, rec, hit, g, L, m);
-#else
-  return shade_by_material(S, max_depth, p, rec, hit, g, L, m);
-#endif
 }
 
 __device__ __forceinline__ bool shade(const DScene& S, int max_depth, Path& p, const Hit& rec, bool hit, Rng& g,

@@ -21,30 +21,13 @@ namespace rtxd {
 
 constexpr int kBlock = 256;
 
-#ifndef RTX_TRACE_WAVES
-#define RTX_TRACE_WAVES 4  // min waves per SIMD for the trace kernels (<= 128 VGPRs; measured best)
-#endif
-#ifndef RTX_FAST_TREE
-#define RTX_FAST_TREE 1  // A/B r01: +2% C2/bunny, +6% C5.  BVH4 source: 0 the reference's SAH tree, 1 our 3-axis SAH tree with 1-prim leaves
-#endif
-#ifndef RTX_BVH4
-#define RTX_BVH4 1  // fast precision traverses the 4-wide collapse of the SAH tree (else BVH2)
-#endif
-#ifndef RTX_SLOT_TARGET_LOG2
-#define RTX_SLOT_TARGET_LOG2 29  // persistent: up to 2^this slots (pixel x sample) per launch, Lbuf <= 12.9 GB (A/B r01: 27 vs 25 = +4% C2, +10% bunny; r02: 29 vs 27 = +4.0% C4, +1.3% C5)
-#endif
-#ifndef RTX_STAMPS
-#define RTX_STAMPS 0  // diagnostic build: s_memtime per region of k_persistent -> counters[24..27]
-#endif
-#ifndef RTX_EARLY_MAT
-#define RTX_EARLY_MAT 0  // persistent: material fetched by the id the traversal kept, beside the record (A/B r01: -2% C2, +-0 bunny)
-#endif
-#ifndef RTX_REFILL_MIN
-#define RTX_REFILL_MIN 24  // persistent lanes: refill once this many lanes of a wave are idle (A/B: ab_refill2_*)
-#endif
-#ifndef RTX_REFILL_MIN_PARK
-#define RTX_REFILL_MIN_PARK 16  // the same for the PARK kernel
-#endif
+// Tuned constants (DESIGN.md ledger: each picked by A/B, the alternatives removed).
+constexpr int kTraceWaves = 4;  // min waves per SIMD for the trace kernels (<= 128 VGPRs; 3 and 5 slower)
+constexpr int kSlotTargetLog2 = 29;  // persistent: up to 2^29 slots (pixel x sample) per launch (r02: 2^29 vs 2^27 C4 +4.0 %, C5 +1.3 %), capped by free memory
+constexpr int kRefillMin = 24;      // persistent lanes: refill once this many lanes of a wave are idle (ab_refill2_*)
+constexpr int kRefillMinPark = 16;  // the same for the PARK kernel
+constexpr int kParkAt = 16;  // PARK kernel: park traversals once at most this many lanes still walk (ab_parkT_*)
+constexpr int kChunk = 256;  // persistent: slots taken per atomic on a region's slot counter (ab_chunk_*)
 
 // Pixel subset of the image handled by one call (rectangle or interleaved row stripes).
 struct PixelMap {
@@ -82,6 +65,11 @@ struct RenderArgs {
   int64_t npix;         // pixels in the subset
   int32_t K;            // samples in this group
   int32_t s0;           // first sample index of the group
+  // Which slots the persistent kernel draws: uniform groups (smap == nullptr), slot p * K + k
+  // is sample s0 + k of pixel p; adaptive phases (render_adaptive), slot i is sample smap[i].y
+  // of pixel smap[i].x, for i below the phase's slot count, which the slot counters' block holds
+  // after the 8 region counters (next_slot[8 * 16], written by k_adapt_expand).
+  const uint2* smap;
   int32_t max_depth;
   int32_t scatter_api;  // megakernel (Scatter/GetPixel) semantics
   const uint8_t* conv;  // per-pixel converged flag (adaptive), may be null
@@ -122,48 +110,37 @@ __device__ __forceinline__ int64_t wave_compact(bool want, unsigned int* counter
 // LDS of a block's traversal stacks: STACK + 1 slots per lane (the branchless pushes of the
 // lean walk may store one slot above the deepest entry, see trace4_run).
 constexpr size_t stack_lds_bytes(int STACK) { return (size_t)(STACK + 1) * kBlock * sizeof(uint32_t); }
-#ifndef RTX_THR_LDS
-#define RTX_THR_LDS 1  // persistent: path throughput parked in LDS across the traversal (no VGPR spill of it)
-#endif
-#ifndef RTX_LAZY_MAT
-#define RTX_LAZY_MAT 1  // persistent (merged shading): material fields read at their use
-#endif
-#ifndef RTX_DEFER_F
-#define RTX_DEFER_F 0  // persistent, texture-free builds: the BSDF albedo read at the end of shading (no gain over RTX_LAZY_MAT)
-#endif
-#ifndef RTX_HITP_LDS
-#define RTX_HITP_LDS 1  // persistent, texture-free builds: the hit point parked in LDS across the BSDF sampling
-#endif
-// The persistent kernel's LDS per block: the traversal stacks (stack_slots per lane, the
-// walk's exact bound + 1), then each lane's path throughput (RTX_THR_LDS) and hit point
-// (RTX_HITP_LDS), 3 doubles each, channel-major (lane-consecutive 8-byte words: conflict-
-// free).  Shading reads the throughput only at its end and the hit point only as the next
-// origin, so both stay in LDS while the lane walks the tree and samples the BSDF instead of
-// occupying 12 of the 128 VGPRs a lane has at 4 waves per SIMD (or spilling to scratch).
-constexpr int kLdsThr = RTX_THR_LDS ? 3 : 0, kLdsHitP = RTX_HITP_LDS ? 3 : 0;
-// The PARK kernel with the speculative walk (RTX_LEAF_SPEC) keeps 16-bit stack entries and
-// adds each lane's leaf queue, RTX_LEAF_SPEC words, after the hit point.
-constexpr size_t persistent_lds_bytes(int stack_slots, bool park = false) {
-  const bool spec = park && RTX_LEAF_SPEC > 0;
-  return (size_t)stack_slots * kBlock * (spec ? sizeof(uint16_t) : sizeof(uint32_t)) +
-         (size_t)(kLdsThr + kLdsHitP) * kBlock * sizeof(double) +
-         (spec ? (size_t)RTX_LEAF_SPEC * kBlock * sizeof(uint32_t) : 0);
+// The persistent kernel's LDS per block: the traversal stacks (stack_slots per lane, the walk's
+// exact bound + 1), then each lane's path throughput and hit point, 3 doubles each,
+// channel-major (lane-consecutive 8-byte words: conflict-free).  Shading reads the throughput
+// only at its end and the hit point only as the next origin, so both stay in LDS while the
+// lane walks the tree and samples the BSDF instead of occupying 12 of the 128 VGPRs a lane has
+// at 4 waves per SIMD (or spilling to scratch).  The PARK kernel with the speculative walk
+// (RTX_LEAF_SPEC) keeps 16-bit stack entries and adds each lane's leaf queue, RTX_LEAF_SPEC
+// 32-bit words, after the hit point.
+//
+// Every region is lane-interleaved with its own element size (2, 8 or 4 bytes), so a lane's
+// words in one region are OTHER lanes' words — lanes of other waves, which run concurrently —
+// in any region it overlapped.  Regions must therefore never share bytes, even where one
+// lane's uses of them never overlap in time: a 6-word leaf queue laid over the hit-point
+// words faulted this way in round 2 (cmp_spec6_fault.txt, ledger).  persist_lds() is the one
+// statement of the layout, used by the kernel and the launch; rtx_internal_lds_layout exposes it
+// to a CPU test that checks the regions are disjoint and inside the block's LDS.
+struct PersistLds {
+  uint32_t stack, thr, hitp, leafq, end;  // byte offsets of the regions in a block's LDS, its size
+};
+constexpr bool spec_walk(bool park, bool fast, bool scatter) { return park && fast && !scatter && RTX_LEAF_SPEC > 0; }
+constexpr PersistLds persist_lds(int stack_slots, bool spec) {
+  const uint32_t stack_bytes = (uint32_t)stack_slots * kBlock * (spec ? 2u : 4u);
+  const uint32_t thr = stack_bytes, hitp = thr + 3u * kBlock * 8u, leafq = hitp + 3u * kBlock * 8u;
+  return PersistLds{0u, thr, hitp, leafq, leafq + (spec ? (uint32_t)RTX_LEAF_SPEC * kBlock * 4u : 0u)};
 }
 
 template <int STACK, bool FAST, bool COUNT, int TK = -1>
 __device__ __forceinline__ int64_t trace(const DScene& S, V3 o, V3 d, double tmin, double tmax, uint32_t* stk,
                                          Counters& c, double& t_best, int32_t& mat_best) {
-#if RTX_BVH4
-#if RTX_NODE_LEAN
   if (FAST) return trace_fast4_lean<STACK, COUNT, TK>(S, o, d, tmin, tmax, stk, kBlock, c, t_best, mat_best);
-#else
-  if (FAST) return trace_fast4<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best, mat_best);
-#endif
   const int64_t b = trace_parity<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best);
-#else
-  const int64_t b = FAST ? trace_fast<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best)
-                         : trace_parity<STACK, COUNT>(S, o, d, tmin, tmax, stk, kBlock, c, t_best);
-#endif
   mat_best = b >= 0 ? S.prims[b].material : -1;
   return b;
 }
@@ -183,11 +160,6 @@ __device__ __forceinline__ void flush_counters(const RenderArgs& A, const Counte
     atomicAdd(&A.counters[5], (unsigned long long)c.wprims);
     atomicAdd(&A.counters[6], (unsigned long long)c.tris);
     atomicAdd(&A.counters[7], (unsigned long long)c.sphs);
-#if RTX_TAILHIST
-    for (int i = 0; i < 6; i++) atomicAdd(&A.counters[40 + i], (unsigned long long)c.tail[i]);
-    for (int i = 0; i < 4; i++) atomicAdd(&A.counters[46 + i], (unsigned long long)c.leafph[i]);
-    atomicAdd(&A.counters[50], (unsigned long long)c.leaft);
-#endif
   }
   if (segs) atomicAdd(&A.counters[0], (unsigned long long)segs);
   if (prims) atomicAdd(&A.counters[1], (unsigned long long)prims);
@@ -197,7 +169,7 @@ __device__ __forceinline__ void flush_counters(const RenderArgs& A, const Counte
 // IntersectBatch
 // ---------------------------------------------------------------------------------------
 template <int STACK, bool FAST>
-__global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_intersect(DScene S, const rtx_ray* __restrict__ rays,
+__global__ __launch_bounds__(kBlock, kTraceWaves) void k_intersect(DScene S, const rtx_ray* __restrict__ rays,
                                                                        int64_t n, rtx_hit* __restrict__ hits,
                                                                        double tmin, double tmax) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -264,7 +236,7 @@ __global__ __launch_bounds__(kBlock) void k_wf_generate(RenderArgs A, PathQueue 
 
 // Closest hit for every queued path (one ray per lane, grid-stride).
 template <int STACK, bool FAST, bool COUNT>
-__global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_wf_extend(RenderArgs A, PathQueue q,
+__global__ __launch_bounds__(kBlock, kTraceWaves) void k_wf_extend(RenderArgs A, PathQueue q,
                                                                        const unsigned int* count) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* stk = lds + threadIdx.x;
@@ -330,86 +302,64 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in,
 // (miss, emitter, absorption, Russian roulette) are immediately given a new primary —
 // the per-wave __ballot of idle lanes is the active-ray compaction.
 // ---------------------------------------------------------------------------------------
-#ifndef RTX_PARK
-#define RTX_PARK 16  // persistent (PARK kernel): park traversals once at most this many lanes still walk (A/B r01: 16 best for the bunny; 0: no PARK kernel)
-#endif
-#ifndef RTX_XCD_REGIONS
-#define RTX_XCD_REGIONS 1  // persistent: slots drawn from 8 per-XCD-group regions (image bands) instead of one counter (A/B r02: C3 +2.9 %, C2 +2.3 %, C4 +2.7 %)
-#endif
-#ifndef RTX_CHUNK
-#define RTX_CHUNK 256  // persistent: slots taken per atomic on the global slot counter
-#endif
-constexpr int kChunk = RTX_CHUNK;
-
 // TK >= 0: every primitive in the fast tree has kind TK (the ground sphere is a global
 // primitive, so the bunny's tree holds triangles, the final and mixed scenes' spheres), so
 // the walk's leaf tests are compiled for that kind alone.
 template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK = -1, bool LAMB = false,
           bool NOTEX = false, bool NODOF = false>
-__global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderArgs A, unsigned long long* next_slot) {
+__global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A, unsigned long long* next_slot) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  // the speculative PARK walk's layout (= persistent_lds_bytes(.., PARK) for every launched PARK build:
-  // the host launches PARK kernels only for fast, non-scatter renders)
-  constexpr bool kSpecLds = PARK && FAST && !SCATTER && RTX_BVH4 && RTX_NODE_LEAN && RTX_PARK > 0 && RTX_LEAF_SPEC > 0;
-  uint32_t* stk = lds + threadIdx.x;
-  uint16_t* stk16 = (uint16_t*)lds + threadIdx.x;  // (kSpecLds)
+  // the LDS layout (persist_lds: the launch sizes it the same way; the host launches PARK
+  // kernels only for fast, non-scatter renders)
+  constexpr bool kSpecLds = spec_walk(PARK, FAST, SCATTER);
+  const PersistLds lay = persist_lds(A.stack_slots, kSpecLds);
+  char* const ldsb = (char*)lds;
+  uint32_t* stk = (uint32_t*)(ldsb + lay.stack) + threadIdx.x;
+  uint16_t* stk16 = (uint16_t*)(ldsb + lay.stack) + threadIdx.x;  // (kSpecLds)
   (void)stk16;
-  double* thr_lds = (double*)(lds + A.stack_slots * (kSpecLds ? kBlock / 2 : kBlock)) + threadIdx.x;  // [c * kBlock]
-  double* hitp_lds = thr_lds + kLdsThr * kBlock;  // [c * kBlock] (RTX_HITP_LDS)
-  uint32_t* leafq = (uint32_t*)(hitp_lds - threadIdx.x + kLdsHitP * kBlock) + threadIdx.x;  // (kSpecLds)
+  double* thr_lds = (double*)(ldsb + lay.thr) + threadIdx.x;    // [c * kBlock]
+  double* hitp_lds = (double*)(ldsb + lay.hitp) + threadIdx.x;  // [c * kBlock]
+  uint32_t* leafq = (uint32_t*)(ldsb + lay.leafq) + threadIdx.x;  // (kSpecLds)
   (void)leafq;
   // nothing else reads rec.p (textured builds: once the texture lookups moved before the sampling)
-  constexpr bool kHitpLds = RTX_HITP_LDS && (NOTEX || RTX_EARLY_TEX) && !SCATTER && RTX_MERGED_SHADE;
+  constexpr bool kHitpLds = (NOTEX || RTX_EARLY_TEX) && !SCATTER;
   (void)hitp_lds;
-  const uint64_t nslots = (uint64_t)A.npix * (uint64_t)A.K;
+  const uint64_t nslots = A.smap ? (uint64_t)next_slot[8 * 16] : (uint64_t)A.npix * (uint64_t)A.K;
   // GetPixel uses Interval(0.001, inf) (camera.h:158); IntersectBatch uses 0.001f (cpu_ray_integrator.h:21)
   const double tmin = SCATTER ? 0.001 : (double)0.001f;
   Counters c{};
   uint32_t segs = 0, prims = 0;
   uint64_t chunk_base = 0, chunk_left = 0;  // wave-uniform
   bool exhausted = false;                   // wave-uniform
-  uint32_t region = blockIdx.x & 7;         // wave-uniform (RTX_XCD_REGIONS)
-  (void)region;
+  uint32_t region = blockIdx.x & 7;         // wave-uniform
   bool has = false;
   Path P;
   P.depth = 0;
   uint32_t slot = 0;           // < nslots <= 2^32 - 1 (host check)
   uint32_t pix = 0, smp = 0;  // RNG identity of the lane's path: global pixel, sample
-  // A traversal still running when at most RTX_PARK lanes of the wave are left walking is
+  // A traversal still running when at most kParkAt lanes of the wave are left walking is
   // parked (trace4_run) and resumed in the next segment round, so the wave goes on to shade
   // the finished lanes instead of idling behind a few long walks.
   // (PARK instantiation only: the host picks it per scene, see rtx_render_device.)
-  constexpr bool kPark = PARK && FAST && !SCATTER && RTX_BVH4 && RTX_NODE_LEAN && RTX_PARK > 0;
+  constexpr bool kPark = PARK && FAST && !SCATTER;
   const bool park_ok = kPark && A.S.use_bvh && !A.S.froot_leaf;
   bool parked = false;
   TravState trs;
-#if RTX_STAMPS
-  uint64_t cyc[4] = {0, 0, 0, 0};
-  uint64_t ts = __builtin_amdgcn_s_memtime();
-#define RTX_STAMP(i)                                   \
-  {                                                    \
-    const uint64_t t_ = __builtin_amdgcn_s_memtime();  \
-    cyc[i] += t_ - ts;                                 \
-    ts = t_;                                           \
-  }
-#else
-#define RTX_STAMP(i)
-#endif
   while (true) {
     // ---- refill: ballot of idle lanes, leftover of the current chunk first.  Refilling
-    // only once RTX_REFILL_MIN lanes are idle (or the wave is empty) amortises the
+    // only once kRefillMin lanes are idle (or the wave is empty) amortises the
     // primary-generation code over several lanes.
     const unsigned long long idle = __ballot(!has);
     bool fresh = false;
-    constexpr int kRefillMin = kPark ? RTX_REFILL_MIN_PARK : RTX_REFILL_MIN;
-    if (idle != 0 && !exhausted && (__popcll(idle) >= kRefillMin || idle == ~0ull)) {
+    constexpr int kRefill = kPark ? kRefillMinPark : kRefillMin;
+    if (idle != 0 && !exhausted && (__popcll(idle) >= kRefill || idle == ~0ull)) {
       const uint64_t nidle = (uint64_t)__popcll(idle);
       const uint64_t rank = (uint64_t)__popcll(idle & ((1ull << lane_id()) - 1ull));
       uint64_t cand = ~0ull;
       if (chunk_left >= nidle) {
         if (!has) cand = chunk_base + rank;
         chunk_base += nidle, chunk_left -= nidle;
-      } else if (RTX_XCD_REGIONS) {
+      } else {
         // the slot range is cut into 8 contiguous regions (bands of the image), one counter
         // each; a wave drains the region of its XCD group (blockIdx % 8: blocks b and b + 8
         // share an XCD and its L2), then moves on to the next ones (load balance at the end).
@@ -433,45 +383,32 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
         } else {
           chunk_left = 0, exhausted = true;
         }
-      } else {
-        unsigned long long nb = 0;
-        if (lane_id() == 0) nb = atomicAdd(next_slot, (unsigned long long)kChunk);
-        nb = __shfl(nb, 0);
-        if (!has) {
-          if (rank < chunk_left) cand = chunk_base + rank;
-          else if (nb < nslots) cand = nb + (rank - chunk_left);
-        }
-        if (nb < nslots) {
-          const uint64_t used = nidle - chunk_left;
-          chunk_base = nb + used, chunk_left = kChunk - used;
-        } else {
-          chunk_left = 0, exhausted = true;
-        }
       }
       if (cand < nslots) slot = (uint32_t)cand, fresh = true;
     }
     // ---- start the primary path of a freshly assigned slot ----
     if (fresh) {
       // nslots < 2^32 (checked on the host): 32-bit division
-      const uint32_t p = (uint32_t)slot / (uint32_t)A.K;
+      uint32_t p, s;
+      if (A.smap) {
+        const uint2 e = A.smap[slot];
+        p = e.x, s = e.y;
+      } else {
+        p = (uint32_t)slot / (uint32_t)A.K;
+        s = (uint32_t)A.s0 + ((uint32_t)slot - p * (uint32_t)A.K);
+      }
       if (!(A.conv && A.conv[p])) {
-        const int k = (int)((uint32_t)slot - p * (uint32_t)A.K);
         int x, y;
         A.map.xy(p, x, y);
-        pix = (uint32_t)(y * A.map.W + x), smp = (uint32_t)(A.s0 + k);
+        pix = (uint32_t)(y * A.map.W + x), smp = s;
         Rng g = make_rng(A.seed, pix, smp, 0u);
         get_ray<NODOF>(A.cam, x, y, g, P.o, P.d);
-#if RTX_THR_LDS
         thr_lds[0] = 1.0, thr_lds[kBlock] = 1.0, thr_lds[2 * kBlock] = 1.0;
-#else
-        P.thr = v3(1.0, 1.0, 1.0);
-#endif
         P.depth = SCATTER ? A.max_depth : 0;
         has = true;
         prims++;
       }
     }
-    RTX_STAMP(0)
     if (!__any(has)) {
       if (exhausted) break;
       continue;
@@ -496,9 +433,9 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
         // parking only when some lane of this round finishes first: every round makes progress
         const bool done =
             kSpecLds ? trace4_run_spec<STACK, COUNT, TK>(A.S, P.o, P.d, tmin, stk16, leafq, kBlock, c, trs,
-                                                         active > RTX_PARK ? RTX_PARK : -1)
+                                                         active > kParkAt ? kParkAt : -1)
                      : trace4_run<STACK, COUNT, TK>(A.S, P.o, P.d, tmin, stk, kBlock, c, trs,
-                                                    active > RTX_PARK ? RTX_PARK : -1);
+                                                    active > kParkAt ? kParkAt : -1);
         parked = !done;
         if (parked) continue;
         best = trs.best, tb = trs.closest, bmat = trs.mat;
@@ -507,22 +444,13 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
       } else {
         best = trace<STACK, FAST, COUNT, TK>(A.S, P.o, P.d, tmin, kInf, stk, c, tb, bmat);
       }
-      RTX_STAMP(1)
       segs++;
       Hit h;
       rtx_material m;
-#if RTX_EARLY_MAT
-      // the material load is in flight together with the winner's record (finish_hit_at)
-      if (best >= 0) m = A.S.mats[bmat];
-#endif
       if (best >= 0) finish_hit_at<false>(A.S, best, tb, P.o, P.d, h);
       if (kHitpLds && best >= 0) hitp_lds[0] = h.p.x, hitp_lds[kBlock] = h.p.y, hitp_lds[2 * kBlock] = h.p.z;
-#if !RTX_EARLY_MAT
       if (best >= 0) m = A.S.mats[h.mat];
-#endif
-#if RTX_THR_LDS
       if (SCATTER) P.thr = v3(thr_lds[0], thr_lds[kBlock], thr_lds[2 * kBlock]);
-#endif
       // stream of this segment: depth + 1 (GetPixel: depth counts down from max_depth)
       Rng g = make_rng(A.seed, pix, smp, SCATTER ? (uint32_t)(A.max_depth - P.depth) + 1u : (uint32_t)P.depth + 1u);
       if (SCATTER) {
@@ -544,64 +472,37 @@ __global__ __launch_bounds__(kBlock, RTX_TRACE_WAVES) void k_persistent(RenderAr
             cont = false;
           }
         }
+        if (cont) thr_lds[0] = P.thr.x, thr_lds[kBlock] = P.thr.y, thr_lds[2 * kBlock] = P.thr.z;
       } else {
-#if RTX_THR_LDS && RTX_MERGED_SHADE
         // the throughput is read from LDS only after the shading core: none of its registers
-        // are live across the walk or the BSDF sampling
+        // are live across the walk or the BSDF sampling; the material's fields are read where
+        // shading uses them (a reference into the table, not a copy loaded up front and held
+        // across the sampling)
         ShadeOut so;
-        constexpr bool kDeferF = NOTEX && RTX_DEFER_F;
-#if RTX_LAZY_MAT
-        // the material's fields are read where shading uses them (a reference into the table,
-        // not a copy loaded up front and held across the sampling)
         const rtx_material& mr = *opaque(A.S.mats + (best >= 0 ? h.mat : 0));
-        shade_core<LAMB, NOTEX, !kHitpLds, kDeferF>(A.S, A.max_depth, P, h, best >= 0, g, mr, so);
-#else
-        shade_core<LAMB, NOTEX, !kHitpLds, kDeferF>(A.S, A.max_depth, P, h, best >= 0, g, m, so);
-#endif
+        shade_core<LAMB, NOTEX, !kHitpLds>(A.S, A.max_depth, P, h, best >= 0, g, mr, so);
         V3 thr = v3(thr_lds[0], thr_lds[kBlock], thr_lds[2 * kBlock]);
         cont = shade_finish(so, thr, P.depth, g, L, best >= 0 ? A.S.mats + h.mat : A.S.mats);
         if (cont) thr_lds[0] = thr.x, thr_lds[kBlock] = thr.y, thr_lds[2 * kBlock] = thr.z;
         if (kHitpLds && cont) P.o = v3(hitp_lds[0], hitp_lds[kBlock], hitp_lds[2 * kBlock]);
-#else
-#if RTX_THR_LDS
-        P.thr = v3(thr_lds[0], thr_lds[kBlock], thr_lds[2 * kBlock]);
-#endif
-        cont = shade<LAMB, NOTEX>(A.S, A.max_depth, P, h, best >= 0, g, L, m);
-#endif
       }
-#if RTX_THR_LDS
-      if (SCATTER && cont) thr_lds[0] = P.thr.x, thr_lds[kBlock] = P.thr.y, thr_lds[2 * kBlock] = P.thr.z;
-#endif
     }
-    RTX_STAMP(2)
     if (!cont) {
       store_radiance(A, slot, L);
       has = false;
     }
   }
-  RTX_STAMP(3)
-#if RTX_STAMPS
-  if (lane_id() == 0)
-    for (int i = 0; i < 4; i++) atomicAdd(&A.counters[24 + i], (unsigned long long)cyc[i]);
-#endif
-#undef RTX_STAMP
   flush_counters(A, c, segs, prims, COUNT);
 }
 
 // The PARK instantiations are compiled in their own translation unit (rtx_park.hip), with
 // their own macro defaults (the leaf-step walk, the branchless triangle test) and scheduler
 // options (Makefile PARKFLAGS; the LLVM default since the leaf-step walk, `ab_sch_c3.txt`).
-#ifndef RTX_PARK_TU
-#define RTX_PARK_TU 1
-#endif
 #define RTX_PARK_INSTANCES(X) \
   X(32, false, false) X(32, true, false) X(64, false, false) X(64, true, false) \
   X(32, false, true) X(32, true, true) X(64, false, true) X(64, true, true)
-#ifndef RTX_TREE_KIND
-#define RTX_TREE_KIND 1  // PARK kernel specialised for triangle-only trees
-#endif
 #define RTX_PARK_TRI_INSTANCES(Y) Y(32) Y(64)
-#if RTX_PARK_TU && !defined(RTX_PERSISTENT_ONLY)
+#ifndef RTX_PERSISTENT_ONLY
 #define RTX_PARK_EXTERN(ST, CO, SC) \
   extern template __global__ void k_persistent<ST, true, CO, SC, true>(RenderArgs, unsigned long long*);
 RTX_PARK_INSTANCES(RTX_PARK_EXTERN)
@@ -664,6 +565,173 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(PixelSoA px, const double
   px.samples[p] = n;
   px.conv[p] = conv;
 }
+
+// ---------------------------------------------------------------------------------------
+// Adaptive sampling in phases (the reference's default mode: WavefrontRenderer::Render,
+// wavefront.cc:42-43 kRelThresh / kMinSamples, converged pixels skipped at :68-69,
+// RecordSample + IsConverged at :125-127 and pixel_state.h:22-72).
+//
+// Phase 1 traces the min_spp samples every pixel needs (uniform slots).  After each phase,
+// k_adapt_record replays RecordSample / IsConverged over the phase's samples of every pixel in
+// sample order (k_accumulate's arithmetic) and, for a pixel neither converged nor out of
+// budget, sizes its next batch from its running statistics: IsConverged holds at n samples once
+// sqrt(var / n) / max(|mean|, 1e-3) <= rel in every channel, i.e. n >= var / (rel mu)^2, so the
+// batch is that many more samples (with a margin that grows with the phase, at least 4, a
+// multiple of 4, within the budget and the workspace).  k_adapt_expand then lays out the next
+// phase's slots, pixel-major, from a prefix sum of the batch sizes, each slot holding its
+// (pixel, sample).  Only pixels still sampling get slots.  A sample traced past its pixel's
+// convergence point is discarded here, so the result is the reference's whatever the batch
+// sizes are: the prediction only decides how much work is spent and how many phases it takes.
+// ---------------------------------------------------------------------------------------
+struct AdaptPlan {
+  const uint32_t* kcur;  // samples of sub-pixel q in the phase just traced (nullptr: kuni each)
+  const uint32_t* off;   // their first slot (nullptr: the uniform first phase, p * kuni)
+  uint32_t* knext;       // out: samples of q in the next phase (0: q is finished)
+  int32_t kuni;
+  int32_t sub_n, sub_j;  // pixel p = q * sub_n + sub_j
+  int32_t min_spp, budget, phase, kcap;
+  double rel;
+};
+__device__ __forceinline__ uint32_t adapt_next_batch(const double (&mean)[3], const double (&m2)[3], int n,
+                                                     const AdaptPlan& ap) {
+  double need = 0.0;  // samples at which IsConverged would hold with the current estimates
+  for (int c = 0; c < 3; c++) {
+    const double var = n > 1 ? m2[c] / (n - 1) : 0.0;
+    const double mu = fmax(fabs(mean[c]), 1e-3);
+    need = fmax(need, var / (ap.rel * ap.rel * mu * mu));
+  }
+  const int left = ap.budget - n;
+  const double margin = 1.0 + 0.25 * (double)(ap.phase - 1);
+  const double want = (need - (double)n) * margin;
+  int k = (want < (double)left) ? (int)ceil(want) : left;  // NaN / inf: the whole budget
+  k = max(k, min(4 << min(ap.phase - 1, 4), left));  // at least 4, 8, ... 64 more
+  k = (k + 3) & ~3;
+  return (uint32_t)min(k, min(left, ap.kcap));
+}
+// One wave per 64 consecutive sub-pixels.  Their batches are runs of the phase's slots in
+// pixel order, so the wave streams the slot range they span through LDS in chunks of
+// kRecChunk slots (coalesced 8-byte loads, the next chunk's loads in flight while the current
+// one is replayed), and each lane replays its own pixel's samples of the chunk in sample order.
+// The wave stops streaming once no lane needs a later sample (converged pixels stop early).
+constexpr int kRecWave = 64, kRecChunk = 256, kRecLoads = 3 * kRecChunk / kRecWave;
+__global__ __launch_bounds__(kRecWave) void k_adapt_record(PixelSoA px, const double* __restrict__ L, int64_t nq,
+                                                           int64_t npix, AdaptPlan ap) {
+  __shared__ double st[3 * kRecChunk];
+  const int t = threadIdx.x;
+  const int64_t q0 = (int64_t)blockIdx.x * kRecWave, q = q0 + t;
+  const bool inq = q < nq;
+  const int64_t p = q * ap.sub_n + ap.sub_j;
+  int K = 0;
+  int64_t o = 0;
+  if (inq) {
+    K = ap.kcur ? (int)ap.kcur[q] : ap.kuni;
+    o = ap.off ? (int64_t)ap.off[q] : p * (int64_t)ap.kuni;
+  }
+  bool live = inq && K > 0 && !px.conv[p];
+  double sum[3] = {0, 0, 0}, mean[3] = {0, 0, 0}, m2[3] = {0, 0, 0};
+  int n = 0;
+  bool conv = false;
+  if (live) {
+    for (int c = 0; c < 3; c++) sum[c] = px.sum[c * npix + p], mean[c] = px.mean[c * npix + p], m2[c] = px.m2[c * npix + p];
+    n = px.samples[p];
+  }
+  // the slots the wave's batches span (runs in q order; the uniform first phase interleaves
+  // the other sub-renders' pixels, which are loaded and skipped)
+  const int last = (int)min<int64_t>(kRecWave - 1, nq - 1 - q0);
+  const int64_t lo = __shfl(o, 0), hi = __shfl(o + K, last);
+  const double* __restrict__ src = L + 3 * lo;
+  const int64_t nd = 3 * (hi - lo);  // doubles in the range
+  double v[kRecLoads];
+  auto load = [&](int64_t d0) {
+#pragma unroll
+    for (int i = 0; i < kRecLoads; i++) {
+      const int64_t e = d0 + t + (int64_t)kRecWave * i;
+      if (e < nd) v[i] = src[e];
+    }
+  };
+  if (nd > 0) load(0);
+  for (int64_t c0 = lo; c0 < hi; c0 += kRecChunk) {
+#pragma unroll
+    for (int i = 0; i < kRecLoads; i++) st[t + kRecWave * i] = v[i];
+    __syncthreads();
+    const int64_t c1 = c0 + kRecChunk;
+    if (c1 < hi) load(3 * (c1 - lo));
+    if (live && !conv) {
+      const int64_t s1 = min<int64_t>(o + K, c1);
+      for (int64_t sl = max<int64_t>(o, c0); sl < s1 && !conv; sl++) {
+        // RecordSample (pixel_state.h:22-39), then IsConverged (pixel_state.h:54-72)
+        const double* x = st + 3 * (sl - c0);
+        n++;
+        for (int c = 0; c < 3; c++) {
+          double mu = mean[c];
+          double delta = x[c] - mu;
+          mu += delta / n;
+          double delta2 = x[c] - mu;
+          mean[c] = mu;
+          m2[c] += delta2 * delta;
+        }
+        for (int c = 0; c < 3; c++) sum[c] += x[c];
+        if (n >= ap.min_spp) {
+          bool ok = true;
+          for (int c = 0; c < 3 && ok; c++) {
+            double var = n > 1 ? m2[c] / (n - 1) : 0.0;
+            double mu = fmax(fabs(mean[c]), 1e-3);
+            double err = sqrt(var) / sqrt((double)n);
+            if (err / mu > ap.rel) ok = false;
+          }
+          conv = ok;
+        }
+      }
+    }
+    __syncthreads();
+    if (__ballot(live && !conv && o + K > c1) == 0) break;  // no lane needs a later slot
+  }
+  if (!inq) return;
+  uint32_t kn = 0;
+  if (live) {
+    for (int c = 0; c < 3; c++) px.sum[c * npix + p] = sum[c], px.mean[c * npix + p] = mean[c], px.m2[c * npix + p] = m2[c];
+    px.samples[p] = n;
+    px.conv[p] = conv;
+    if (!conv && n < ap.budget) kn = adapt_next_batch(mean, m2, n, ap);
+  }
+  ap.knext[q] = kn;
+}
+// The next phase's slot map: sub-pixel q's batch occupies slots [off[q], off[q] + knext[q]),
+// slot off[q] + k being sample samples[p] + k of pixel p.  One block per 256 sub-pixels; its
+// slots are a contiguous range written by all its threads (coalesced), each finding its
+// sub-pixel by a search of the block's offsets in LDS.  The last sub-pixel's thread writes the
+// phase's slot count.
+__global__ __launch_bounds__(kBlock) void k_adapt_expand(const uint32_t* __restrict__ knext,
+                                                         const uint32_t* __restrict__ off, int64_t nq, int32_t sub_n,
+                                                         int32_t sub_j, const int32_t* __restrict__ samples,
+                                                         uint2* __restrict__ smap,
+                                                         unsigned long long* __restrict__ total) {
+  __shared__ uint32_t s_off[kBlock], s_p[kBlock], s_s0[kBlock];
+  __shared__ uint32_t s_end;
+  const int t = threadIdx.x;
+  const int64_t q0 = (int64_t)blockIdx.x * kBlock, q = q0 + t;
+  const int nb = (int)min<int64_t>(kBlock, nq - q0);
+  if (t < nb) {
+    const uint32_t k = knext[q], o = off[q];
+    const int64_t p = q * sub_n + sub_j;
+    s_off[t] = o, s_p[t] = (uint32_t)p, s_s0[t] = k ? (uint32_t)samples[p] : 0u;
+    if (t == nb - 1) {
+      s_end = o + k;
+      if (q == nq - 1) *total = (unsigned long long)o + k;
+    }
+  }
+  __syncthreads();
+  const uint32_t b = s_off[0], e = s_end;
+  for (uint32_t i = b + t; i < e; i += kBlock) {
+    int lo = 0, hi = nb;  // the last q with s_off[q] <= i (a zero batch shares its successor's offset)
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (s_off[mid] <= i) lo = mid;
+      else hi = mid;
+    }
+    smap[i] = make_uint2(s_p[lo], s_s0[lo] + (i - s_off[lo]));
+  }
+}
 #endif
 
 // Fixed-spp accumulation: the sum RecordSample (and DefaultSampler) forms, in sample order.
@@ -672,16 +740,9 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(PixelSoA px, const double
 // each pixel's contiguous run of 3 * kAccChunk doubles with 16-byte loads (8-byte loads when
 // the runs are not 16-byte aligned, i.e. K odd, or for a short last chunk), all issued before
 // the first LDS store, then each lane adds its own pixel's samples in order.
-#ifndef RTX_ACC_CHUNK
-#define RTX_ACC_CHUNK 8  // samples per LDS-staged chunk of the fixed-spp accumulate (with 16 pixels per workgroup; ab_acc*)
-#endif
-#ifndef RTX_ACC_PIPE
-#define RTX_ACC_PIPE 1  // accumulate: the next chunk's loads are in flight while the current one is summed
-#endif
-#ifndef RTX_ACC_PIX
-#define RTX_ACC_PIX 16  // accumulate: pixels per 64-lane workgroup (fewer: less LDS, more workgroups per CU; ab_acc*)
-#endif
-constexpr int kAccWave = 64, kAccPix = RTX_ACC_PIX, kAccChunk = RTX_ACC_CHUNK,
+// 8-sample chunks, 16 pixels per 64-lane workgroup (LDS 3.1 KB; ab_acc*), the next chunk's
+// loads in flight while the current one is summed (ab_acc_pipe).
+constexpr int kAccWave = 64, kAccPix = 16, kAccChunk = 8,
               kAccPitch = 3 * kAccChunk + 1;  // odd pitch: spread LDS banks
 static_assert(kAccPix <= kAccWave, "one summing lane per pixel");
 #ifndef RTX_PERSISTENT_ONLY  // rtx_park.hip: the persistent kernel's PARK instantiations only
@@ -708,7 +769,6 @@ __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const 
   double sum[3] = {0, 0, 0};
   if (t < npx && !first)
     for (int c = 0; c < 3; c++) sum[c] = px.sum[c * npix + p];
-#if RTX_ACC_PIPE
   // Full chunks with 16-byte-aligned runs (K even) are software-pipelined: chunk i + 1 is
   // loaded into registers before chunk i is summed out of LDS.  Same adds, same order.
   constexpr int PP = 3 * kAccChunk / 2;  // 16-byte pieces per pixel run
@@ -740,9 +800,6 @@ __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const 
     }
   }
   for (int k0 = kfull; k0 < K; k0 += kAccChunk) {
-#else
-  for (int k0 = 0; k0 < K; k0 += kAccChunk) {
-#endif
     const int kc = std::min(kAccChunk, K - k0);
     if (kc == kAccChunk && (K & 1) == 0) {
       constexpr int PP = 3 * kAccChunk / 2;  // 16-byte pieces per pixel run

@@ -27,7 +27,6 @@
 #include "rtx.h"
 #include "rtx_kernels.h"
 
-#if RTX_PARK_TU  // else rtx_capi.hip instantiates them itself
 namespace rtxd {
 #define RTX_PARK_DEFINE(ST, CO, SC) \
   template __global__ void k_persistent<ST, true, CO, SC, true>(RenderArgs, unsigned long long*);
@@ -43,4 +42,3 @@ RTX_PARK_INSTANCES(RTX_PARK_DEFINE)
 RTX_PARK_TRI_INSTANCES(RTX_PARK_TRI_DEFINE)
 #undef RTX_PARK_TRI_DEFINE
 }  // namespace rtxd
-#endif

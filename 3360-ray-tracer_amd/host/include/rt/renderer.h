@@ -53,7 +53,7 @@ class WavefrontRenderer {
   std::vector<double> rgb_;
   std::vector<int32_t> spp_;
   rtx_stats stats_{};
-  std::vector<int> devices_;          // extra devices (besides the integrator's)
+  std::vector<int> devices_;          // the frame's devices, the integrator's first (set_devices)
   std::vector<rtx_scene*> extra_;     // their device-resident copies of the scene
   int stripe_rows_ = 8;
 };

@@ -11,8 +11,8 @@ Workloads (BASELINE.json configs): the default is the north-star scene, the Stan
   * N GPUs: C4, bunny 3840x2160, 1024 spp, depth 50, the SAME frame split over the N ranks
     (strong scaling): the image's rows are interleaved 8-row stripes, stripe k -> rank k mod N
     (SURVEY §8e); every rank copies its stripes into one shared host framebuffer
-    (/dev/shm); no collective touches the data path (RCCL only carries the timing barrier
-    and the max-over-ranks reduction).
+    (/dev/shm); no collective touches the data path (a gloo process group carries only the
+    timing barrier and the max-over-ranks reduction).
 Other workloads: --workload c2_final | c5_mixed | c1_three | c4_bunny4k | c3_bunny.
 
 Prints ONE JSON line (rank 0).  `roofline` prices the dominant kernel (k_persistent) against
@@ -53,6 +53,7 @@ N_SIMD, CLOCK_HZ, LANES_PER_CYCLE, CYCLES_PER_VALU = 1024, 2.4e9, 16, 4
 VALU_PEAK_LANE_OPS = N_SIMD * LANES_PER_CYCLE * CLOCK_HZ  # 39.3e12 lane-ops/s
 HBM_PEAK_GBS = 8000.0
 STRIPE_ROWS = 8
+ADAPTIVE_MIN_SPP, ADAPTIVE_REL = 16, float(np.float32(0.05))  # wavefront.cc:42-43 (kRelThresh is a float)
 
 
 def available_cpus():
@@ -122,10 +123,16 @@ def main():
                          "plain/park force one (identical results; used by scripts/profile.sh so the "
                          "trace holds no schedule-timing launches)")
     ap.add_argument("--generic", action="store_true", help="time the generic (unspecialised) kernel build")
+    ap.add_argument("--adaptive", action="store_true",
+                    help="the reference's default sampling (wavefront.cc:42-43, 62-69, 125-127): per-pixel "
+                         "adaptive, at least 16 samples, relative error 0.05f, up to the workload's spp")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-generic-leg", action="store_true", help="skip the generic-build comparison frames")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--dist-backend", default="nccl", help="nccl (=RCCL, one GPU per rank) or gloo (rehearsal)")
+    ap.add_argument("--dist-backend", default="gloo",
+                    help="process group of the N>1 timing barrier and max/sum reductions: gloo (default; no "
+                         "collective touches the data path, so the host-side group the 1-GPU rehearsals run is "
+                         "the one an 8-GPU run takes) or nccl (= RCCL)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -158,7 +165,8 @@ def main():
 
     def params(flags=sched_flags, generic=False):
         p = rtx.RenderParams()
-        p.spp, p.max_depth, p.adaptive, p.seed = spp, depth, 0, args.seed
+        p.spp, p.max_depth, p.adaptive, p.seed = spp, depth, int(args.adaptive), args.seed
+        p.min_spp, p.rel_threshold = ADAPTIVE_MIN_SPP, ADAPTIVE_REL
         p.mode, p.precision = rtx.MODES[args.mode], rtx.PRECISIONS[args.precision]
         p.stripe_rows, p.stripe_index, p.stripe_count = STRIPE_ROWS, rank, world
         p.flags = flags | (rtx.RTX_FLAG_GENERIC if generic else 0)
@@ -270,6 +278,7 @@ def main():
     if rank == 0:
         out = {
             "metric": "Mrays/s (primary+secondary) at fixed spp; RMS pixel error vs CPU ref",
+            "sampling": sampling_text(args.adaptive),
             "value": rays_all / elapsed / 1e6,
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -281,7 +290,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": f"{workload}: {scene_name} scene {W}x{H}, {spp} spp, depth {depth}, fixed spp"
+            "config": {"workload": f"{workload}: {scene_name} scene {W}x{H}, {spp} spp, depth {depth}, "
+                                   + sampling_text(args.adaptive)
                                    + (f", one frame split over {world} GPUs" if world > 1 else ""),
                        "scene_prims": int(host.desc().n_prims), "bvh_nodes": int(host.desc().n_nodes),
                        "mode": args.mode, "precision": args.precision,
@@ -306,13 +316,18 @@ def main():
         dist.destroy_process_group()
 
 
+def sampling_text(adaptive):
+    return (f"adaptive (min {ADAPTIVE_MIN_SPP} spp, rel. error 0.05f, max = spp)" if adaptive else "fixed spp")
+
+
 def valu_roofline(workload, args, segs_per_launch, avg_launch_s):
     """VALU-issue roofline of the hot kernel from the committed PMC profile of this build.
 
     useful lane-ops / segment = SQ_INSTS_VALU x 64 x lane utilisation / segments, where lane
     utilisation = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU) (PMC, same launch); achieved =
     that x segments per launch (this run) / average launch time (this run, HIP events)."""
-    pf = os.path.join(ROOT, "profiles", f"valu_{workload}_{args.mode}_{args.precision}.json")
+    pf = os.path.join(ROOT, "profiles", f"valu_{workload}_{args.mode}_{args.precision}"
+                      + ("_adaptive" if args.adaptive else "") + ".json")
     base = {"bound": "valu", "peak": VALU_PEAK_LANE_OPS / 1e12, "unit": "Tlane-op/s (VALU)"}
     if not os.path.exists(pf):
         return {**base, "achieved": None, "frac": None, "traffic": None, "note": f"no PMC profile {pf}"}
@@ -352,27 +367,27 @@ def cpu_baseline(rtx, dev, host, cam, preset, scene_name, spp, depth, args, park
         # probe on a small centre band (twice: the first call also starts the thread pool),
         # then size the timed sample to ~15 s of wall time, capped at the whole frame
         probe = (0, H // 2 - 2, W, 4)
+        ad = dict(adaptive=int(args.adaptive), rng="philox", mode="per_pixel", threads=threads)
         for _ in range(2):
             t0 = time.perf_counter()
-            s.render(cfg, W, spp, depth, args.seed, adaptive=0, rng="philox", mode="per_pixel", tile=probe,
-                     threads=threads)
+            s.render(cfg, W, spp, depth, args.seed, tile=probe, **ad)
             per_row = (time.perf_counter() - t0) / 4
         ch = int(max(4, min(H, 15.0 / max(per_row, 1e-6))))
         tile = (0, max(0, H // 2 - ch // 2), W, ch)
         t0 = time.perf_counter()
-        ref, _, st = s.render(cfg, W, spp, depth, args.seed, adaptive=0, rng="philox", mode="per_pixel", tile=tile,
-                              threads=threads)
+        ref, ref_spp, st = s.render(cfg, W, spp, depth, args.seed, tile=tile, **ad)
         dt = time.perf_counter() - t0
     sched = "park" if parked else "plain"
-    gpu, _, gst = dev.render(cam, spp, depth, seed=args.seed, adaptive=False, tile=tile, mode=args.mode,
-                             precision=args.precision, schedule=sched if args.mode == "persistent" else None,
-                             generic=args.generic)
+    gpu, gpu_spp, gst = dev.render(cam, spp, depth, seed=args.seed, adaptive=args.adaptive, tile=tile, mode=args.mode,
+                                   precision=args.precision, schedule=sched if args.mode == "persistent" else None,
+                                   generic=args.generic, min_spp=ADAPTIVE_MIN_SPP, rel_threshold=ADAPTIVE_REL)
     rms = float(np.sqrt(np.mean((gpu - ref.reshape(-1, 3)) ** 2)))
     what = "the whole" if ch == H else f"centre band {W}x{ch} of the same"
     base = {"value": st["rays"] / dt / 1e6, "unit": "Mrays/s", "cores": threads, "nproc": os.cpu_count(),
             "kind": "port",
             "sample": f"{what} {W}x{H} frame, {spp} spp, depth {depth}, fixed spp, "
-                      f"{st['rays']} segments in {dt:.1f}s (oracle/rtx_oracle.cc, OpenMP on {threads} threads, philox)"}
+                      f"{st['rays']} segments in {dt:.1f}s (oracle/rtx_oracle.cc, OpenMP on {threads} threads, philox)"
+                      .replace("fixed spp", sampling_text(args.adaptive))}
     cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
     if os.path.exists(cal):
         c = json.load(open(cal))
@@ -388,7 +403,14 @@ def cpu_baseline(rtx, dev, host, cam, preset, scene_name, spp, depth, args, park
                         "reference_equivalent_value = value / ratio estimates the reference on these cores"}
     check = {"mode": args.mode, "precision": args.precision, "schedule": sched,
              "kernel_build": rtx.build_names(gst["build"]), "same_build_as_timed": gst["build"] == build_bits,
-             "rows": [tile[1], tile[1] + tile[3]]}
+             "rows": [tile[1], tile[1] + tile[3]],
+             "sample_counts_identical": bool(np.array_equal(gpu_spp, ref_spp.ravel())),
+             "segments_gpu": int(gst["rays_total"]), "segments_cpu": int(st["rays"])}
+    if args.adaptive:
+        check["pixels_converged_early"] = float(np.mean(ref_spp < spp))
+        check["mean_spp"] = float(np.mean(ref_spp))
+        # whole sample groups are traced; samples past a pixel's convergence are discarded
+        check["recorded_fraction_of_traced_segments"] = st["rays"] / max(1, gst["rays_total"])
     return base, rms, check
 
 

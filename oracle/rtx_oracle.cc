@@ -1257,6 +1257,29 @@ int orc_intersect(void* sp, const double* rays, long long n, double tmin, double
   }
   return 0;
 }
+// Every primitive whose own closest hit on the ray (hit_prim on (tmin, inf): the near root
+// first, as Scene::Hit would report it) lies at exactly distance t: up to `cap` records of
+// 12 doubles (the orc_intersect layout), brute force over the whole primitive list.  Returns
+// how many there are.  Test hook: a fast-precision closest hit that differs from the
+// parity one must be an exact t tie between distinct primitives (tests/test_gpu_parity.py).
+int orc_tied_hits(void* sp, const double* ray, double tmin, double t, double* out, int cap) {
+  Scene* s = (Scene*)sp;
+  double tm = tmin < 0 ? (double)0.001f : tmin;
+  V3 o{ray[0], ray[1], ray[2]}, d{ray[3], ray[4], ray[5]};
+  int n = 0;
+  for (const Prim& p : s->prims) {
+    Hit rec;
+    if (!hit_prim(p, o, d, tm, kInf, rec) || rec.t != t) continue;
+    if (n < cap) {
+      double* q = out + 12 * n;
+      q[0] = 1, q[1] = rec.t, q[2] = rec.p.x, q[3] = rec.p.y, q[4] = rec.p.z;
+      q[5] = rec.normal.x, q[6] = rec.normal.y, q[7] = rec.normal.z;
+      q[8] = rec.u, q[9] = rec.v, q[10] = rec.front_face, q[11] = rec.mat;
+    }
+    n++;
+  }
+  return n;
+}
 int orc_aabb(const double* cases, long long n, int* out) {
   for (long long i = 0; i < n; i++) {
     const double* q = cases + 14 * i;

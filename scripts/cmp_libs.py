@@ -27,6 +27,8 @@ CASES = [  # scene recipe, camera preset, width, spp, depth, mode, precision, ad
     ("bunny", "c3_bunny", 160, 16, 20, "persistent", "fast", False, "park"),  # the PARK kernel, forced
     ("mixed", "c5_mixed", 96, 8, 50, "persistent", "fast", False, "park"),
     ("cornell", "cornell", 64, 16, 50, "persistent", "fast", False, "park"),
+    ("bunny", "c3_bunny", 400, 64, 20, "persistent", "fast", True),  # adaptive, two sub-renders
+    ("final", "c2_final", 400, 48, 50, "persistent", "fast", True),
 ]
 
 
@@ -67,7 +69,9 @@ def main():
         rays_same = int(outs[0][f"rays{i}"][0]) == int(outs[1][f"rays{i}"][0])
         report[" ".join(map(str, case))] = {"bit_identical": bool(same), "pixels_identical": frac,
                                             "spp_identical": bool(spp_same), "rays_identical": bool(rays_same)}
-        ok &= same and spp_same and rays_same
+        # adaptive renders trace whole batches, so the segments traced (not the result) depend on
+        # the batch schedule
+        ok &= same and spp_same and (rays_same or case[7])
     print(json.dumps(report, indent=1))
     print("ALL BIT-IDENTICAL" if ok else "DIFFERENCES FOUND")
     return 0 if ok else 1

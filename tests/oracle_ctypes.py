@@ -48,6 +48,7 @@ def lib():
         L.orc_scene_bvh.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         L.orc_intersect.argtypes = [C.c_void_p, C.c_void_p, C.c_longlong, C.c_double, C.c_void_p, C.c_int]
         L.orc_aabb.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p]
+        L.orc_tied_hits.argtypes = [C.c_void_p, C.c_void_p, C.c_double, C.c_double, C.c_void_p, C.c_int]
         L.orc_material.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p, C.c_int]
         L.orc_texture.argtypes = [C.c_void_p, C.c_longlong, C.c_char_p, C.c_void_p]
         L.orc_pixelstate.argtypes = [C.c_void_p, C.c_longlong, C.c_void_p]
@@ -116,6 +117,14 @@ class Scene:
         out = np.zeros((len(rays), 12))
         lib().orc_intersect(self.h, _ptr(rays), len(rays), tmin, _ptr(out), threads)
         return out
+
+    def tied_hits(self, ray, t, tmin=-1.0, cap=16):
+        """Records (12 doubles, the intersect layout) of every primitive whose own closest hit
+        on `ray` is at exactly distance t (brute force over all primitives)."""
+        ray = np.ascontiguousarray(ray, dtype=np.float64).reshape(6)
+        out = np.zeros((cap, 12))
+        n = lib().orc_tied_hits(self.h, _ptr(ray), tmin, t, _ptr(out), cap)
+        return out[:min(n, cap)], n
 
     def render(self, cam_cfg, width, spp, max_depth, seed, adaptive=1, rng="philox", mode="per_pixel",
                tile=None, threads=1, mk_min_samples=0, mk_threshold=0.0):

@@ -57,3 +57,26 @@ def test_invalid_descriptors_rejected_before_launch(rtx_mod):
     h = C.c_void_p()
     rc = rtx_mod.lib().rtx_scene_create(0, C.byref(d), C.byref(h))
     assert rc == -1 and b"material out of range" in rtx_mod.lib().rtx_last_error()
+
+
+@pytest.mark.parametrize("park", [0, 1])
+def test_persistent_lds_regions_are_disjoint(rtx_mod, park):
+    """The persistent kernel's LDS regions (traversal stacks, throughput, hit point, leaf queue)
+    are each lane-interleaved with their own element size, so a byte shared by two regions
+    belongs to DIFFERENT lanes in the two — lanes of other waves that run concurrently.  Round 2's
+    6-word leaf queue laid over the hit-point words faulted exactly that way (ledger,
+    cmp_spec6_fault.txt).  The layout the kernel and the launch share (persist_lds, exported as a
+    host-only test hook) must keep every region inside the block's LDS and apart from the others,
+    for every stack size the host can choose (the lean walk's exact bound + 1, up to 65)."""
+    f = rtx_mod.lib().rtx_internal_lds_layout
+    f.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_uint32)]
+    out = (C.c_uint32 * 9)()
+    for slots in range(1, 66):
+        assert f(slots, park, out) == 0
+        stack, thr, hitp, leafq, end, *per_lane = list(out)
+        regions = [(o, o + 256 * b) for o, b in zip((stack, thr, hitp, leafq), per_lane) if b]
+        regions.sort()
+        assert regions[0][0] == 0 and regions[-1][1] == end, (slots, regions, end)
+        for (a0, a1), (b0, b1) in zip(regions, regions[1:]):
+            assert a1 <= b0, (slots, regions)
+        assert thr % 8 == 0 and hitp % 8 == 0 and end <= 160 * 1024, (slots, thr, hitp, end)  # a workgroup may take all 160 KiB

@@ -62,8 +62,14 @@ def test_intersect_parity_bit_exact(dev_scenes, scene):
 
 
 @pytest.mark.parametrize("scene", ["final", "bunny", "mixed", "cornell"])
-def test_intersect_fast_matches_parity(dev_scenes, scene):
-    """f32 conservative traversal + f64 primitive tests: same closest hits."""
+def test_intersect_fast_matches_parity(dev_scenes, orc, mixed_scene_file, scene):
+    """f32 conservative traversal + f64 primitive tests: the same closest hit as the parity
+    walk (the reference's Bvh::Hit order), except where two distinct primitives hit at exactly
+    the same distance and the walks meet them in a different order.  Every ray whose fast and
+    parity records differ is checked to be such a tie: both report the same t, bit for bit,
+    and the oracle's brute force over all primitives (the reference's own hit arithmetic)
+    finds at least two primitives at that t, among whose records are both the fast and the
+    parity record."""
     z = np.load(os.path.join(GOLDEN, f"hits_{scene}.npz"))
     d = dev_scenes(scene)
     rng = np.random.default_rng(5)
@@ -71,8 +77,18 @@ def test_intersect_fast_matches_parity(dev_scenes, scene):
     a = hit_matrix(d.intersect(rays, precision="parity"))
     b = hit_matrix(d.intersect(rays, precision="fast"))
     cols = [0, 1, 2, 3, 4, 5, 6, 7, 10, 11]
-    same = np.all(a[:, cols] == b[:, cols], 1)
-    assert same.mean() >= 0.9995, np.nonzero(~same)[0][:5]
+    differ = np.nonzero(~np.all(a[:, cols] == b[:, cols], 1))[0]
+    osc = orc.Scene(mixed_scene_file if scene == "mixed" else scene_path(scene)) if len(differ) else None
+    for i in differ:
+        assert a[i, 0] == 1 and b[i, 0] == 1, ("hit/miss mismatch", i, a[i], b[i])
+        assert a[i, 1] == b[i, 1], ("closest distances differ", i, a[i, 1], b[i, 1])
+        tied, n = osc.tied_hits(rays[i], a[i, 1])
+        assert n >= 2, ("not a tie", i, n, a[i], b[i])
+        recs = tied[:, cols]
+        assert np.any(np.all(recs == a[i, cols], 1)) and np.any(np.all(recs == b[i, cols], 1)), (i, tied, a[i], b[i])
+    # ties are rare (coincident surfaces, shared triangle edges): a regression that culls real
+    # hits shows up as hundreds of non-tie mismatches above, not as a rate
+    assert len(differ) <= 0.01 * len(rays), len(differ)
 
 
 @pytest.mark.parametrize("n_small", [3, 12])
@@ -207,6 +223,28 @@ def test_group_size_does_not_change_results(rtx_mod, dev_scenes):
         for mode in ("wavefront", "persistent"):
             rgb, sp, _ = d.render(cam, 40, 20, seed=3, adaptive=True, samples_per_group=K, mode=mode)
             assert np.array_equal(rgb, ref) and np.array_equal(sp, rspp), (K, mode)
+
+
+@pytest.mark.parametrize("scene,preset,w,spp,depth,schedule", [("final", "c2_final", 400, 40, 50, None),
+                                                               ("bunny", "c3_bunny", 400, 64, 20, "park"),
+                                                               ("cornell", "cornell", 300, 48, 20, "plain"),
+                                                               ("three", "c1_three", 64, 24, 4, None)])
+def test_adaptive_phases_equal_uniform_groups(rtx_mod, dev_scenes, scene, preset, w, spp, depth, schedule):
+    # (the Cornell box is too noisy for any pixel to converge within 48 samples: every pixel
+    # takes the whole budget through the phases' growing batches)
+    """Adaptive persistent renders run in phases (render_adaptive: per-pixel batch sizes
+    predicted from each pixel's statistics, slot maps, two interleaved sub-renders on two
+    streams from 2^16 pixels up): the same pixels and sample counts, bit for bit, as uniform
+    groups of 4 samples over every pixel."""
+    cam = rtx_mod.camera(rtx_mod.camera_config(preset, width=w))
+    d = dev_scenes(scene)
+    kw = dict(seed=17, adaptive=True, mode="persistent", precision="fast", schedule=schedule)
+    a, sa, sta = d.render(cam, spp, depth, **kw)
+    b, sb, stb = d.render(cam, spp, depth, samples_per_group=4, **kw)
+    assert np.array_equal(sa, sb), np.nonzero(sa != sb)[0][:5]
+    assert np.array_equal(a, b)
+    assert sa.min() >= min(16, spp) and sa.max() <= spp and ((sa < spp).any() or scene == "cornell")
+    assert sta["rays_primary"] >= sa.sum() and stb["rays_primary"] >= sa.sum()
 
 
 def test_edge_cases(rtx_mod, dev_scenes, tmp_path, gpu):

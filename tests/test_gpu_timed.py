@@ -80,6 +80,44 @@ def test_timed_kernel_builds_match_oracle(rtx_mod, orc, scenes, case, schedule):
     assert np.all(sp == spp) and st["rays_total"] == ref_st["rays"]
 
 
+# The reference's default sampling (WavefrontRenderer::Render is always adaptive:
+# wavefront.cc:42-43 kRelThresh 0.05f / kMinSamples 16, converged pixels skipped at :68-69,
+# IsConverged at :125-127), on the timed builds at the configurations' own cameras and
+# widths: full-width row bands, with the configurations' sample budgets where the oracle
+# finishes in seconds (C2 100, C3 200 spp) and 64 spp for the 4K ones.
+ADAPTIVE_CASES = [  # bench case index, spp, band rows
+    (0, 100, 2),
+    (1, 200, 2),
+    (2, 64, 1),
+    (3, 64, 1),
+]
+ADAPTIVE_MIN, ADAPTIVE_REL = 16, float(np.float32(0.05))
+
+
+@pytest.mark.parametrize("schedule", ["plain", "park", "auto"])
+@pytest.mark.parametrize("acase", ADAPTIVE_CASES, ids=[BENCH_CASES[c[0]][1] for c in ADAPTIVE_CASES])
+def test_timed_kernel_builds_adaptive_match_oracle(rtx_mod, orc, scenes, acase, schedule):
+    """Per-pixel sample counts equal the oracle's exactly, pixels within RMS_TOL: whatever
+    the group schedule traces past a pixel's convergence is discarded, never recorded."""
+    ci, spp, rows = acase
+    scene, preset, width, _, depth, plain_build, park_build = BENCH_CASES[ci]
+    path, d = scenes(scene)
+    cam = rtx_mod.camera(rtx_mod.camera_config(preset, width=width))
+    tile = (0, cam.image_height // 2 - rows, cam.image_width, rows)
+    ref, ref_spp, ref_st = oracle(orc, path, preset, width, spp, depth, 515, tile, adaptive=1)
+    rgb, sp, st = d.render(cam, spp, depth, seed=515, adaptive=True, mode="persistent", precision="fast", tile=tile,
+                           schedule=schedule, min_spp=ADAPTIVE_MIN, rel_threshold=ADAPTIVE_REL)
+    names = set(rtx_mod.build_names(st["build"])) & SPECIALISED
+    want = {"plain": plain_build, "park": park_build}.get(schedule) or (park_build if st["parked"] else plain_build)
+    assert names == want, (names, want)
+    ref_spp = ref_spp.ravel()
+    assert np.array_equal(sp, ref_spp), (np.nonzero(sp != ref_spp)[0][:5], sp[sp != ref_spp][:5])
+    assert ref_spp.min() >= ADAPTIVE_MIN and ref_spp.max() <= spp
+    assert st["rays_total"] >= ref_st["rays"] and st["rays_primary"] >= ref_st["primaries"]
+    rms = np.sqrt(np.mean((rgb - ref.reshape(-1, 3)) ** 2))
+    assert rms <= RMS_TOL, rms
+
+
 @pytest.mark.parametrize("case", BENCH_CASES, ids=[c[1] for c in BENCH_CASES])
 def test_generic_build_equals_specialised(rtx_mod, scenes, case):
     """Specialisation compiles out unreachable code only: identical pixels and counts."""
