@@ -111,8 +111,9 @@ constexpr int kBands = 8;  // bands of the last accumulate and of the D2H copies
 // phase-end work (the launch tail, the record / scan / expand kernels, the host's look at the
 // next phase's size) overlaps the other's tracing.
 constexpr int kAdaptSubs = 2;
+constexpr int64_t kAdaptPhaseSlots = 1 << 21;  // render_adaptive: smallest phase a sub-render plans while pixels remain
 struct AdaptWs {
-  DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then the slot count (u64)
+  DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address
   HostBuf total_h;                              // pinned copy of the next phase's slot count
   hipStream_t st = nullptr;                     // sub-render 0 runs on the caller's stream
   hipEvent_t ev = nullptr;                      // total_h written
@@ -565,8 +566,9 @@ struct Launch {
   hipStream_t s;
   int stack;
   bool fast, count;
-  bool park = false;  // persistent: the PARK kernel (parked traversals), chosen per scene
+  int park = 0;  // persistent: 0 plain kernel, PARK kernel (parked traversals) with 1 the leaf-step, 2 the speculative walk
   bool generic = false;  // RTX_FLAG_GENERIC: no per-scene specialisation (TK, LAMB, NOTEX, NODOF)
+  bool map = false;      // adaptive phases: slots from the phase's slot map (k_persistent MAP)
   mutable uint32_t build = 0;  // RTX_BUILD_* bits of the persistent instantiation launched last
 };
 
@@ -581,28 +583,37 @@ int run_extend(const Launch& L, const RenderArgs& A, const PathQueue& q, const u
   return RTX_OK;
 }
 
-template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK, bool LAMB = false, bool NOTEX = false,
-          bool NODOF = false>
-int run_persistent_k0(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
+template <int STACK, bool FAST, bool COUNT, bool SCATTER, int PARK, int TK, bool LAMB, bool NOTEX, bool NODOF,
+          bool MAP>
+int run_persistent_k1(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
   if (A.stack_slots < 1 || A.stack_slots > STACK + 1) return fail(RTX_ERR_INVALID, "bad traversal stack size");
   const size_t lds = persist_lds(A.stack_slots, spec_walk(PARK, FAST, SCATTER)).end;
   const int grid = persistent_grid(
-      L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF>, lds);
-  L.build = (PARK ? RTX_BUILD_PARK : 0u) | (TK == (int)RTX_PRIM_SPHERE ? RTX_BUILD_SPHERE_TREE : 0u) |
+      L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF, MAP>, lds);
+  L.build = (PARK ? RTX_BUILD_PARK : 0u) | (PARK == 2 ? RTX_BUILD_SPECULATIVE : 0u) | (TK == (int)RTX_PRIM_SPHERE ? RTX_BUILD_SPHERE_TREE : 0u) |
             (TK == (int)RTX_PRIM_TRIANGLE ? RTX_BUILD_TRIANGLE_TREE : 0u) | (LAMB ? RTX_BUILD_LAMBERTIAN : 0u) |
             (NOTEX ? RTX_BUILD_NO_TEXTURES : 0u) | (NODOF ? RTX_BUILD_NO_DEFOCUS : 0u) |
             (FAST ? RTX_BUILD_FAST : 0u) | (COUNT ? RTX_BUILD_COUNT : 0u) | (SCATTER ? RTX_BUILD_SCATTER : 0u);
   if (std::getenv("RTX_DEBUG_LAUNCH"))
     fprintf(stderr, "rtx launch: k_persistent build 0x%x grid %d (%d blocks per CU) lds %zu B stack_slots %d\n",
             L.build, grid, grid / std::max(1, L.sc->cus), lds, A.stack_slots);
-  hipLaunchKernelGGL((k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF>), dim3(grid),
+  hipLaunchKernelGGL((k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF, MAP>), dim3(grid),
                      dim3(kBlock), lds, L.s, A, next_slot);
   HIPC(hipGetLastError());
   return RTX_OK;
 }
+// adaptive phases draw their slots from a slot map (L.map; never with the scatter API)
+template <int STACK, bool FAST, bool COUNT, bool SCATTER, int PARK, int TK, bool LAMB = false, bool NOTEX = false,
+          bool NODOF = false>
+int run_persistent_k0(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
+  if (!SCATTER && L.map)
+    return run_persistent_k1<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF, !SCATTER>(L, A, next_slot);
+  if (L.map) return fail(RTX_ERR_INVALID, "slot maps are not used with the scatter API");
+  return run_persistent_k1<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF, false>(L, A, next_slot);
+}
 // the texture-free plain build also comes without the camera's thin-lens sampling (defocus
 // off; C2 +1.0 %; the PARK build lost 2.8 % with it, ab_nodof_*)
-template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK, bool LAMB = false, bool NOTEX = false>
+template <int STACK, bool FAST, bool COUNT, bool SCATTER, int PARK, int TK, bool LAMB = false, bool NOTEX = false>
 int run_persistent_k(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
   if (NOTEX && !PARK && A.cam.defocus_angle <= 0)
     return run_persistent_k0<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NOTEX && !PARK>(L, A, next_slot);
@@ -610,7 +621,7 @@ int run_persistent_k(const Launch& L, const RenderArgs& A, unsigned long long* n
 }
 // fast frames of a scene whose tree holds one kind run a build for that kind: triangles with
 // the PARK schedule (the bunny), spheres with the plain one (the final and mixed scenes)
-template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK>
+template <int STACK, bool FAST, bool COUNT, bool SCATTER, int PARK>
 int run_persistent(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
   constexpr bool spec = FAST && !COUNT && !SCATTER;
   constexpr int TK = spec ? (PARK ? (int)RTX_PRIM_TRIANGLE : (int)RTX_PRIM_SPHERE) : -1;
@@ -639,18 +650,21 @@ int extend(const Launch& L, const RenderArgs& A, const PathQueue& q, const unsig
   if (L.fast) return L.count ? extend_s<true, true>(L, A, q, c, n) : extend_s<true, false>(L, A, q, c, n);
   return L.count ? extend_s<false, true>(L, A, q, c, n) : extend_s<false, false>(L, A, q, c, n);
 }
-template <bool FAST, bool COUNT, bool SCATTER, bool PARK>
+template <bool FAST, bool COUNT, bool SCATTER, int PARK>
 int persist_s(const Launch& L, const RenderArgs& A, unsigned long long* ns) {
   return L.stack == 32 ? run_persistent<32, FAST, COUNT, SCATTER, PARK>(L, A, ns)
                        : run_persistent<64, FAST, COUNT, SCATTER, PARK>(L, A, ns);
 }
 template <bool SCATTER>
 int persist_m(const Launch& L, const RenderArgs& A, unsigned long long* ns) {
+  constexpr int kSpec = SCATTER ? 1 : 2;  // (the scatter API never runs the PARK kernel)
+  if (L.fast && L.park == 2 && !SCATTER)
+    return L.count ? persist_s<true, true, SCATTER, kSpec>(L, A, ns) : persist_s<true, false, SCATTER, kSpec>(L, A, ns);
   if (L.fast && L.park && !SCATTER)
-    return L.count ? persist_s<true, true, SCATTER, true>(L, A, ns) : persist_s<true, false, SCATTER, true>(L, A, ns);
+    return L.count ? persist_s<true, true, SCATTER, 1>(L, A, ns) : persist_s<true, false, SCATTER, 1>(L, A, ns);
   if (L.fast)
-    return L.count ? persist_s<true, true, SCATTER, false>(L, A, ns) : persist_s<true, false, SCATTER, false>(L, A, ns);
-  return L.count ? persist_s<false, true, SCATTER, false>(L, A, ns) : persist_s<false, false, SCATTER, false>(L, A, ns);
+    return L.count ? persist_s<true, true, SCATTER, 0>(L, A, ns) : persist_s<true, false, SCATTER, 0>(L, A, ns);
+  return L.count ? persist_s<false, true, SCATTER, 0>(L, A, ns) : persist_s<false, false, SCATTER, 0>(L, A, ns);
 }
 
 int time_park_schedule(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm, hipStream_t s);
@@ -670,7 +684,8 @@ template <class Mark>
 int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const rtx_render_params* prm,
                     const PixelSoA& px, int budget, hipStream_t s, Mark mark, uint64_t& hot_launches) {
   const int64_t npix = A.npix;
-  const int S = npix >= (1 << 16) ? kAdaptSubs : 1;
+  static const char* subs_env = std::getenv("RTX_ADAPT_SUBS");  // tuning: sub-render count (1 or 2)
+  const int S = (npix >= (1 << 16) && !(subs_env && std::atoi(subs_env) == 1)) ? kAdaptSubs : 1;
   const int K1 = std::min(std::max(1, prm->min_spp), budget);
   static const bool debug = std::getenv("RTX_DEBUG_ADAPT") != nullptr;  // per-phase slot counts on stderr
   if ((int64_t)npix * K1 > 0xFFFFFFFFll) return fail(RTX_ERR_INVALID, "adaptive render: npix x min_spp above 2^32");
@@ -691,7 +706,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
       if ((rc = b->reserve(nq[j] * sizeof(uint32_t)))) return rc;
     if ((rc = w.scan_tmp.reserve(std::max<size_t>(16, rtxscan::temp_bytes(nq[j]))))) return rc;
     if ((rc = w.ctr.reserve(8 * 16 * sizeof(unsigned long long) + 64))) return rc;
-    if ((rc = w.total_h.reserve(sizeof(unsigned long long)))) return rc;
+    if ((rc = w.total_h.reserve(2 * sizeof(unsigned long long)))) return rc;
     if (!w.ev) HIPC(hipEventCreateWithFlags(&w.ev, hipEventDisableTiming));
     if (j > 0 && !w.st) HIPC(hipStreamCreateWithFlags(&w.st, hipStreamNonBlocking));
   }
@@ -707,7 +722,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   };
   // record + next batch sizes of sub-render j's pixels after phase g (its slots in L: the
   // uniform first phase's, or the phase's slot map), then the next phase's slot map and count
-  auto record = [&](int j, hipStream_t st, int g, const double* Lph) -> int {
+  auto record = [&](int j, hipStream_t st, int g, const double* Lph, int64_t active) -> int {
     AdaptWs& w = sc->aw[j];
     AdaptPlan ap;
     ap.kcur = g == 1 ? nullptr : w.k[g & 1].as<uint32_t>();
@@ -715,13 +730,17 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ap.knext = w.k[(g + 1) & 1].as<uint32_t>();
     ap.kuni = K1, ap.sub_n = S, ap.sub_j = j;
     ap.min_spp = prm->min_spp, ap.budget = budget, ap.phase = g, ap.kcap = kcap[j];
+    // a phase of at least ~kAdaptPhaseSlots slots while pixels remain: once few pixels are left,
+    // their batches grow (up to the budget) instead of phases that are mostly launch tail
+    ap.kmin = (int32_t)std::min<int64_t>(budget, (kAdaptPhaseSlots + active - 1) / std::max<int64_t>(1, active));
     ap.rel = prm->rel_threshold;
-    hipLaunchKernelGGL(k_adapt_record, dim3((unsigned)((nq[j] + kRecWave - 1) / kRecWave)), dim3(kRecWave), 0, st, px,
-                       Lph, nq[j], npix, ap);
+    ap.active = w.ctr.as<unsigned long long>() + 8 * 16 + 1;
+    hipLaunchKernelGGL(k_adapt_record, dim3((unsigned)((nq[j] + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, px, Lph,
+                       nq[j], npix, ap);
     HIPC(hipGetLastError());
     int rc2;
     if ((rc2 = plan(j, st, ap.knext))) return rc2;
-    HIPC(hipMemcpyAsync(w.total_h.p, w.ctr.as<unsigned long long>() + 8 * 16, sizeof(unsigned long long),
+    HIPC(hipMemcpyAsync(w.total_h.p, w.ctr.as<unsigned long long>() + 8 * 16, 2 * sizeof(unsigned long long),
                         hipMemcpyDeviceToHost, st));
     HIPC(hipEventRecord(w.ev, st));
     return RTX_OK;
@@ -733,13 +752,24 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     RenderArgs A1 = A;
     A1.L = sc->lbuf.as<double>();
     A1.conv = nullptr;
-    A1.K = K1, A1.s0 = 0, A1.smap = nullptr;
+    A1.K = K1, A1.s0 = 0;
     unsigned long long* ctr = sc->aw[0].ctr.as<unsigned long long>();
     HIPC(hipMemsetAsync(ctr, 0, 8 * 16 * sizeof(unsigned long long), s));
+    if (debug) HIPC(hipEventRecord(sc->ev[2], s));
     if ((rc = mark(s))) return rc;
     if ((rc = persist_m<false>(L, A1, ctr))) return rc;
     if ((rc = mark(s))) return rc;
     hot_launches++;
+    if (debug) {
+      HIPC(hipEventRecord(sc->ev[3], s));
+      HIPC(hipEventSynchronize(sc->ev[3]));
+      float ms = 0;
+      unsigned long long seg1 = 0;
+      HIPC(hipEventElapsedTime(&ms, sc->ev[2], sc->ev[3]));
+      HIPC(hipMemcpy(&seg1, A.counters, sizeof seg1, hipMemcpyDeviceToHost));
+      fprintf(stderr, "rtx adaptive: phase 1: %lld pixels x %d samples, launch %.3f ms, %llu segments (%.0f Mseg/s)\n",
+              (long long)npix, K1, ms, seg1, (double)seg1 / (ms * 1e3));
+    }
   }
   if (S > 1) {  // the sub-renders' streams start once the first phase is done
     for (hipEvent_t* e : {&sc->fork_ev, &sc->join_ev})
@@ -749,7 +779,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   }
   bool alive[kAdaptSubs] = {false, false};
   for (int j = 0; j < S; j++) {
-    if ((rc = record(j, j == 0 ? s : sc->aw[j].st, 1, sc->lbuf.as<double>()))) return rc;
+    if ((rc = record(j, j == 0 ? s : sc->aw[j].st, 1, sc->lbuf.as<double>(), nq[j]))) return rc;
     alive[j] = true;
   }
   for (int g = 2; alive[0] || alive[1]; g++) {
@@ -760,8 +790,9 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
       unsigned long long* ctr = w.ctr.as<unsigned long long>();  // 8 region counters, then the slot count
       // this phase's slot count, computed at the end of the previous one
       HIPC(hipEventSynchronize(w.ev));
-      const unsigned long long nsl = *(const volatile unsigned long long*)w.total_h.p;
-      if (debug) fprintf(stderr, "rtx adaptive: sub-render %d phase %d: %llu slots\n", j, g, nsl);
+      const unsigned long long nsl = ((const volatile unsigned long long*)w.total_h.p)[0];
+      const int64_t active = (int64_t)((const volatile unsigned long long*)w.total_h.p)[1];
+      if (debug) fprintf(stderr, "rtx adaptive: sub-render %d phase %d: %lld pixels, %llu slots\n", j, g, (long long)active, nsl);
       if (nsl == 0) {
         alive[j] = false;
         continue;
@@ -769,16 +800,32 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
       RenderArgs Aj = A;
       Aj.L = w.lbuf.as<double>();
       Aj.conv = nullptr;  // only pixels still sampling have slots
-      Aj.K = 1, Aj.s0 = 0;
-      Aj.smap = w.smap.as<uint2>();
+      Aj.K = 1, Aj.s0 = 0;  // (unused: slots from the phase's slot map)
       Launch Lj = L;
       Lj.s = st;
+      Lj.map = true;
       HIPC(hipMemsetAsync(ctr, 0, 8 * 16 * sizeof(unsigned long long), st));
+      unsigned long long seg0 = 0;
+      if (debug) {
+        HIPC(hipStreamSynchronize(st));
+        HIPC(hipMemcpy(&seg0, A.counters, sizeof seg0, hipMemcpyDeviceToHost));
+        HIPC(hipEventRecord(sc->ev[2], st));
+      }
       if ((rc = mark(st))) return rc;
       if ((rc = persist_m<false>(Lj, Aj, ctr))) return rc;
       if ((rc = mark(st))) return rc;
       hot_launches++;
-      if ((rc = record(j, st, g, Aj.L))) return rc;
+      if (debug) {
+        HIPC(hipEventRecord(sc->ev[3], st));
+        HIPC(hipEventSynchronize(sc->ev[3]));
+        float ms = 0;
+        unsigned long long seg1 = 0;
+        HIPC(hipEventElapsedTime(&ms, sc->ev[2], sc->ev[3]));
+        HIPC(hipMemcpy(&seg1, A.counters, sizeof seg1, hipMemcpyDeviceToHost));
+        fprintf(stderr, "rtx adaptive:   phase %d launch %.3f ms, %llu segments (%.0f Mseg/s; other sub-renders' included)\n",
+                g, ms, seg1 - seg0, (double)(seg1 - seg0) / (ms * 1e3));
+      }
+      if ((rc = record(j, st, g, Aj.L, active))) return rc;
     }
   }
   if (S > 1) {  // s continues once every sub-render is done
@@ -1128,20 +1175,18 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   Launch L{sc, s, fast ? sc->stack_fast : sc->stack_parity, fast, (prm->flags & RTX_FLAG_COUNT) != 0};
   L.generic = (prm->flags & RTX_FLAG_GENERIC) != 0;
   if (fast && prm->mode == RTX_MODE_PERSISTENT) {
-    if (prm->flags & RTX_FLAG_PARK) L.park = true;
-    else if (prm->flags & RTX_FLAG_NO_PARK) L.park = false;
+    bool park;
+    if (prm->flags & RTX_FLAG_PARK) park = true;
+    else if (prm->flags & RTX_FLAG_NO_PARK) park = false;
     else {
       int rc;
       if (sc->park < 0 && (rc = time_park_schedule(sc, cam, prm, s))) return rc;
-      L.park = sc->park == 1;
+      park = sc->park == 1;
     }
-    // the speculative PARK walk keeps 16-bit node indices on its stack: larger trees get the
-    // plain kernel, and a render that asks for the PARK kernel is refused
-    if (RTX_LEAF_SPEC > 0 && sc->n_f4 > 65536) {
-      if (prm->flags & RTX_FLAG_PARK)
-        return fail(RTX_ERR_INVALID, "RTX_FLAG_PARK: the speculative PARK walk takes trees of at most 65536 nodes");
-      L.park = false;
-    }
+    // the speculative walk keeps 16-bit node indices on its stack: larger trees (and renders
+    // that ask for it) get the leaf-step walk
+    const bool spec = sc->n_f4 <= kSpecMaxNodes && !(prm->flags & RTX_FLAG_LEAF_STEP);
+    L.park = park ? (spec ? 2 : 1) : 0;
   }
 
   // samples in flight per pixel (group size K)
@@ -1212,7 +1257,6 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   A.conv = prm->adaptive ? sc->px_conv.as<uint8_t>() : nullptr;
   A.L = sc->lbuf.as<double>();
   A.counters = cnt;
-  A.smap = nullptr;
   // the lean BVH4 walk stores at most fast_need + 1 stack slots (branchless pushes); the
   // parity walk gets its template bound (pick_stack: reference depth + 2)
   A.stack_slots = fast ? sc->fast_need + 1 : L.stack + 1;
@@ -1686,18 +1730,18 @@ extern "C" int rtx_internal_check_sincos(int device, int64_t n, uint64_t seed, i
 }
 
 // Test hook (not in rtx.h): the persistent kernel's LDS layout (persist_lds) for a traversal
-// stack of stack_slots entries per lane, the PARK build (park = 1: its speculative walk when
-// compiled in) or the plain one: out[0..4] = byte offsets of the stack, throughput, hit point,
+// stack of stack_slots entries per lane and a schedule (park: 0 plain, 1 PARK with the
+// leaf-step walk, 2 PARK with the speculative walk): out[0..4] = byte offsets of the stack, throughput, hit point,
 // leaf queue and the block's LDS size; out[5..8] = each region's bytes per lane (entries x
 // element size), the regions being lane-interleaved with stride kBlock.  tests/
 // test_capi_exports.py checks that the regions are disjoint and inside the block's LDS for every
 // stack size the host can choose.
 extern "C" int rtx_internal_lds_layout(int stack_slots, int park, uint32_t* out) {
-  if (stack_slots < 1 || stack_slots > 65 || !out) return fail(RTX_ERR_INVALID, "bad argument");
-  const bool spec = spec_walk(park != 0, true, false);
+  if (stack_slots < 1 || stack_slots > 65 || park < 0 || park > 2 || !out) return fail(RTX_ERR_INVALID, "bad argument");
+  const bool spec = spec_walk(park, true, false);
   const PersistLds l = persist_lds(stack_slots, spec);
   const uint32_t v[9] = {l.stack, l.thr, l.hitp, l.leafq, l.end, (uint32_t)stack_slots * (spec ? 2u : 4u), 24u, 24u,
-                         spec ? (uint32_t)RTX_LEAF_SPEC * 4u : 0u};
+                         spec ? kLeafQueue * 4u : 0u};
   std::memcpy(out, v, sizeof v);
   return RTX_OK;
 }

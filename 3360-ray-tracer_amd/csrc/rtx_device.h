@@ -919,22 +919,18 @@ __device__ __forceinline__ bool trace4_run_step(const DScene& S, V3 o, V3 d, dou
   return done;
 }
 
-#ifndef RTX_LEAF_SPEC
-// PARK kernel: capacity of each lane's leaf queue in LDS for the speculative walk
-// (trace4_run_spec, a power of two >= 8); 0: the leaf-step walk
-#define RTX_LEAF_SPEC 0
-#endif
-#ifndef RTX_LEAF_SPEC_MIN
-#define RTX_LEAF_SPEC_MIN 24  // speculative walk: queued leaves are tested once this many lanes hold some
-#endif
-#ifndef RTX_LEAF_SPEC_WAIT
-#define RTX_LEAF_SPEC_WAIT 0  // 1: lanes that cannot visit wait for the leaf round instead of forcing it
-#endif
+// The speculative walk's leaf queue: kLeafQueue words per lane (a power of two >= 8); a wave
+// tests queued leaves once kLeafSpecMin of its lanes hold some, or no lane can visit a node
+// (r02/ab/ab_spec8_c3.txt, ab_s16spec8_c3.txt: 8 words, forcing at 24 lanes; waiting with 8
+// lanes: the bunny +0.8 % over the leaf-step walk, r03/ab_spec8w_c3.txt)
+constexpr uint32_t kLeafQueue = 8;
+constexpr int kLeafSpecMin = 8;
 // The lean walk with speculative node visits (Aila & Laine 2009, "speculative traversal"):
-// a visit's leaf slots go into the lane's FIFO queue (an LDS column of RTX_LEAF_SPEC words)
-// and the lane walks on; a wave runs leaf tests only when RTX_LEAF_SPEC_MIN lanes hold queued
-// leaves, or some lane cannot go on (its queue might overflow on the next visit, or its walk
-// is over), and then every lane with a queued leaf tests one.  Same result, bit for bit, as
+// a visit's leaf slots go into the lane's FIFO queue (an LDS column of kLeafQueue words) and
+// the lane walks on; a wave runs leaf tests only when kLeafSpecMin lanes hold queued leaves,
+// or no lane can go on (each lane's queue might overflow on the next visit, its walk is over
+// or it is parking), and then every lane with a queued leaf tests one; a lane that cannot
+// visit meanwhile waits.  Same result, bit for bit, as
 // trace4_run: the queue keeps the primitive tests in the order of the visits that found them,
 // and node visits keep their depth-first order, because an entry distance does not depend on
 // the closest hit.  A visit made before earlier leaves were tested culls its children against
@@ -948,7 +944,7 @@ template <int STACK, bool COUNT, int KIND = -1>
 __device__ __forceinline__ bool trace4_run_spec(const DScene& S, V3 o, V3 d, double tmin, uint16_t* stk,
                                                 uint32_t* lq, int stride, Counters& cnt, TravState& ts,
                                                 int park_at) {
-  constexpr uint32_t F = RTX_LEAF_SPEC > 0 ? RTX_LEAF_SPEC : 8;
+  constexpr uint32_t F = kLeafQueue;
   static_assert(F >= 8 && (F & (F - 1)) == 0, "leaf queue: a power of two >= 8");
   FRay4L r = make_fray4l(o, d);
   const char* __restrict__ nbase = (const char*)S.f4nodes;
@@ -981,15 +977,8 @@ __device__ __forceinline__ bool trace4_run_spec(const DScene& S, V3 o, V3 d, dou
       }
       walking = visit_next<STACK, uint16_t>(tt, cc, false, closest, tmax_f, tmax_x, stk, stride, sp, node);
     }
-#if RTX_LEAF_SPEC_WAIT
-    // a lane that cannot visit waits; leaves are tested once enough lanes hold some, or no
-    // lane of the wave can visit a node any more
     const bool can_visit = walking && !park && qn <= F - 4;
-    if (__ballot(can_visit) == 0 || __popcll(__ballot(qn != 0)) >= RTX_LEAF_SPEC_MIN) {
-#else
-    const bool blocked = qn != 0 && (!walking || park || qn > F - 4);
-    if (__ballot(blocked) != 0 || __popcll(__ballot(qn != 0)) >= RTX_LEAF_SPEC_MIN) {
-#endif
+    if (__ballot(can_visit) == 0 || __popcll(__ballot(qn != 0)) >= kLeafSpecMin) {
       if (qn != 0) {  // one queued leaf, in visit order
         const uint32_t cur = lq[qh * stride];
         qh = (qh + 1) & (F - 1), qn--;

@@ -65,11 +65,6 @@ struct RenderArgs {
   int64_t npix;         // pixels in the subset
   int32_t K;            // samples in this group
   int32_t s0;           // first sample index of the group
-  // Which slots the persistent kernel draws: uniform groups (smap == nullptr), slot p * K + k
-  // is sample s0 + k of pixel p; adaptive phases (render_adaptive), slot i is sample smap[i].y
-  // of pixel smap[i].x, for i below the phase's slot count, which the slot counters' block holds
-  // after the 8 region counters (next_slot[8 * 16], written by k_adapt_expand).
-  const uint2* smap;
   int32_t max_depth;
   int32_t scatter_api;  // megakernel (Scatter/GetPixel) semantics
   const uint8_t* conv;  // per-pixel converged flag (adaptive), may be null
@@ -116,8 +111,8 @@ constexpr size_t stack_lds_bytes(int STACK) { return (size_t)(STACK + 1) * kBloc
 // only at its end and the hit point only as the next origin, so both stay in LDS while the
 // lane walks the tree and samples the BSDF instead of occupying 12 of the 128 VGPRs a lane has
 // at 4 waves per SIMD (or spilling to scratch).  The PARK kernel with the speculative walk
-// (RTX_LEAF_SPEC) keeps 16-bit stack entries and adds each lane's leaf queue, RTX_LEAF_SPEC
-// 32-bit words, after the hit point.
+// (PARK = 2) keeps 16-bit stack entries and adds each lane's leaf queue, kLeafQueue 32-bit
+// words, after the hit point.
 //
 // Every region is lane-interleaved with its own element size (2, 8 or 4 bytes), so a lane's
 // words in one region are OTHER lanes' words — lanes of other waves, which run concurrently —
@@ -129,11 +124,15 @@ constexpr size_t stack_lds_bytes(int STACK) { return (size_t)(STACK + 1) * kBloc
 struct PersistLds {
   uint32_t stack, thr, hitp, leafq, end;  // byte offsets of the regions in a block's LDS, its size
 };
-constexpr bool spec_walk(bool park, bool fast, bool scatter) { return park && fast && !scatter && RTX_LEAF_SPEC > 0; }
+// PARK: 0 the plain schedule, 1 the PARK schedule with the leaf-step walk (trace4_run_step),
+// 2 the PARK schedule with the speculative walk (trace4_run_spec; trees of at most
+// kSpecMaxNodes nodes, its stack entries being 16-bit)
+constexpr bool spec_walk(int park, bool fast, bool scatter) { return park == 2 && fast && !scatter; }
+constexpr int64_t kSpecMaxNodes = 65536;
 constexpr PersistLds persist_lds(int stack_slots, bool spec) {
   const uint32_t stack_bytes = (uint32_t)stack_slots * kBlock * (spec ? 2u : 4u);
   const uint32_t thr = stack_bytes, hitp = thr + 3u * kBlock * 8u, leafq = hitp + 3u * kBlock * 8u;
-  return PersistLds{0u, thr, hitp, leafq, leafq + (spec ? (uint32_t)RTX_LEAF_SPEC * kBlock * 4u : 0u)};
+  return PersistLds{0u, thr, hitp, leafq, leafq + (spec ? (uint32_t)kLeafQueue * kBlock * 4u : 0u)};
 }
 
 template <int STACK, bool FAST, bool COUNT, int TK = -1>
@@ -305,8 +304,15 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in,
 // TK >= 0: every primitive in the fast tree has kind TK (the ground sphere is a global
 // primitive, so the bunny's tree holds triangles, the final and mixed scenes' spheres), so
 // the walk's leaf tests are compiled for that kind alone.
-template <int STACK, bool FAST, bool COUNT, bool SCATTER, bool PARK, int TK = -1, bool LAMB = false,
-          bool NOTEX = false, bool NODOF = false>
+// Which slots the kernel draws: uniform groups (MAP = false), slot p * K + k is sample s0 + k
+// of pixel p; adaptive phases (render_adaptive, MAP = true), slot i is sample smap[i].y of
+// pixel smap[i].x for i below the phase's slot count, where the slot counters' block holds,
+// after the 8 region counters, the slot count (next_slot[128]) and the slot map's address
+// (next_slot[130]), both written by k_adapt_expand.  MAP is a template parameter, not a kernel
+// argument: the fixed-spp kernels run at the SGPR limit, and any extra uniform state there
+// reshuffles their register allocation (a runtime switch cost the bunny's build 3.7 %, r3d).
+template <int STACK, bool FAST, bool COUNT, bool SCATTER, int PARK, int TK = -1, bool LAMB = false,
+          bool NOTEX = false, bool NODOF = false, bool MAP = false>
 __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A, unsigned long long* next_slot) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   // the LDS layout (persist_lds: the launch sizes it the same way; the host launches PARK
@@ -324,7 +330,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   // nothing else reads rec.p (textured builds: once the texture lookups moved before the sampling)
   constexpr bool kHitpLds = (NOTEX || RTX_EARLY_TEX) && !SCATTER;
   (void)hitp_lds;
-  const uint64_t nslots = A.smap ? (uint64_t)next_slot[8 * 16] : (uint64_t)A.npix * (uint64_t)A.K;
+  const uint64_t nslots = MAP ? (uint64_t)next_slot[8 * 16] : (uint64_t)A.npix * (uint64_t)A.K;
   // GetPixel uses Interval(0.001, inf) (camera.h:158); IntersectBatch uses 0.001f (cpu_ray_integrator.h:21)
   const double tmin = SCATTER ? 0.001 : (double)0.001f;
   Counters c{};
@@ -341,7 +347,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   // parked (trace4_run) and resumed in the next segment round, so the wave goes on to shade
   // the finished lanes instead of idling behind a few long walks.
   // (PARK instantiation only: the host picks it per scene, see rtx_render_device.)
-  constexpr bool kPark = PARK && FAST && !SCATTER;
+  constexpr bool kPark = PARK > 0 && FAST && !SCATTER;
   const bool park_ok = kPark && A.S.use_bvh && !A.S.froot_leaf;
   bool parked = false;
   TravState trs;
@@ -389,18 +395,14 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
     // ---- start the primary path of a freshly assigned slot ----
     if (fresh) {
       // nslots < 2^32 (checked on the host): 32-bit division
-      uint32_t p, s;
-      if (A.smap) {
-        const uint2 e = A.smap[slot];
-        p = e.x, s = e.y;
-      } else {
-        p = (uint32_t)slot / (uint32_t)A.K;
-        s = (uint32_t)A.s0 + ((uint32_t)slot - p * (uint32_t)A.K);
-      }
+      uint2 e = make_uint2(0u, 0u);
+      if (MAP) e = ((const uint2*)next_slot[8 * 16 + 2])[slot];
+      const uint32_t p = MAP ? e.x : (uint32_t)slot / (uint32_t)A.K;
       if (!(A.conv && A.conv[p])) {
+        const int k = MAP ? 0 : (int)((uint32_t)slot - p * (uint32_t)A.K);
         int x, y;
         A.map.xy(p, x, y);
-        pix = (uint32_t)(y * A.map.W + x), smp = s;
+        pix = (uint32_t)(y * A.map.W + x), smp = MAP ? e.y : (uint32_t)(A.s0 + k);
         Rng g = make_rng(A.seed, pix, smp, 0u);
         get_ray<NODOF>(A.cam, x, y, g, P.o, P.d);
         thr_lds[0] = 1.0, thr_lds[kBlock] = 1.0, thr_lds[2 * kBlock] = 1.0;
@@ -498,22 +500,32 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
 // The PARK instantiations are compiled in their own translation unit (rtx_park.hip), with
 // their own macro defaults (the leaf-step walk, the branchless triangle test) and scheduler
 // options (Makefile PARKFLAGS; the LLVM default since the leaf-step walk, `ab_sch_c3.txt`).
-#define RTX_PARK_INSTANCES(X) \
-  X(32, false, false) X(32, true, false) X(64, false, false) X(64, true, false) \
-  X(32, false, true) X(32, true, true) X(64, false, true) X(64, true, true)
-#define RTX_PARK_TRI_INSTANCES(Y) Y(32) Y(64)
+// (ST: stack size, CO: counting build, SC: scatter API, MP: adaptive slot map, PK: 1 the
+// leaf-step walk, 2 the speculative walk; the host never launches the PARK kernel for the
+// scatter API, nor maps a scatter render's slots, but its dispatch names those builds)
+#define RTX_PARK_INSTANCES(X)                                                                                    \
+  X(32, false, false, false, 1) X(32, true, false, false, 1) X(64, false, false, false, 1)                      \
+  X(64, true, false, false, 1) X(32, false, true, false, 1) X(32, true, true, false, 1)                         \
+  X(64, false, true, false, 1) X(64, true, true, false, 1) X(32, false, false, true, 1)                         \
+  X(32, true, false, true, 1) X(64, false, false, true, 1) X(64, true, false, true, 1)                          \
+  X(32, false, false, false, 2) X(32, true, false, false, 2) X(64, false, false, false, 2)                      \
+  X(64, true, false, false, 2) X(32, false, false, true, 2) X(32, true, false, true, 2)                         \
+  X(64, false, false, true, 2) X(64, true, false, true, 2)
+#define RTX_PARK_TRI_INSTANCES(Y) \
+  Y(32, false, 1) Y(64, false, 1) Y(32, true, 1) Y(64, true, 1) Y(32, false, 2) Y(64, false, 2) Y(32, true, 2) Y(64, true, 2)
 #ifndef RTX_PERSISTENT_ONLY
-#define RTX_PARK_EXTERN(ST, CO, SC) \
-  extern template __global__ void k_persistent<ST, true, CO, SC, true>(RenderArgs, unsigned long long*);
+#define RTX_PARK_EXTERN(ST, CO, SC, MP, PK)                                                                   \
+  extern template __global__ void k_persistent<ST, true, CO, SC, PK, -1, false, false, false, MP>(RenderArgs, \
+                                                                                              unsigned long long*);
 RTX_PARK_INSTANCES(RTX_PARK_EXTERN)
 #undef RTX_PARK_EXTERN
-#define RTX_PARK_TRI_EXTERN(ST)                                                                        \
-  extern template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE, false>(  \
-      RenderArgs, unsigned long long*);                                                                   \
-  extern template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE, true>(   \
-      RenderArgs, unsigned long long*);                                                                   \
-  extern template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE, true, true>( \
-      RenderArgs, unsigned long long*);
+#define RTX_PARK_TRI_EXTERN(ST, MP, PK)                                                                             \
+  extern template __global__ void k_persistent<ST, true, false, false, PK, RTX_PRIM_TRIANGLE, false, false, false, \
+                                               MP>(RenderArgs, unsigned long long*);                              \
+  extern template __global__ void k_persistent<ST, true, false, false, PK, RTX_PRIM_TRIANGLE, true, false, false,  \
+                                               MP>(RenderArgs, unsigned long long*);                              \
+  extern template __global__ void k_persistent<ST, true, false, false, PK, RTX_PRIM_TRIANGLE, true, true, false,   \
+                                               MP>(RenderArgs, unsigned long long*);
 RTX_PARK_TRI_INSTANCES(RTX_PARK_TRI_EXTERN)
 #undef RTX_PARK_TRI_EXTERN
 #endif
@@ -590,7 +602,9 @@ struct AdaptPlan {
   int32_t kuni;
   int32_t sub_n, sub_j;  // pixel p = q * sub_n + sub_j
   int32_t min_spp, budget, phase, kcap;
+  int32_t kmin;  // smallest next batch: keeps a phase with few pixels left large enough to fill the GPU
   double rel;
+  unsigned long long* active;  // the next phase's pixel count (k_adapt_expand adds; zeroed here)
 };
 __device__ __forceinline__ uint32_t adapt_next_batch(const double (&mean)[3], const double (&m2)[3], int n,
                                                      const AdaptPlan& ap) {
@@ -604,91 +618,67 @@ __device__ __forceinline__ uint32_t adapt_next_batch(const double (&mean)[3], co
   const double margin = 1.0 + 0.25 * (double)(ap.phase - 1);
   const double want = (need - (double)n) * margin;
   int k = (want < (double)left) ? (int)ceil(want) : left;  // NaN / inf: the whole budget
-  k = max(k, min(4 << min(ap.phase - 1, 4), left));  // at least 4, 8, ... 64 more
+  k = max(k, min(max(4 << min(ap.phase - 1, 4), ap.kmin), left));  // at least 4, 8, ... 64 more, and kmin
   k = (k + 3) & ~3;
   return (uint32_t)min(k, min(left, ap.kcap));
 }
-// One wave per 64 consecutive sub-pixels.  Their batches are runs of the phase's slots in
-// pixel order, so the wave streams the slot range they span through LDS in chunks of
-// kRecChunk slots (coalesced 8-byte loads, the next chunk's loads in flight while the current
-// one is replayed), and each lane replays its own pixel's samples of the chunk in sample order.
-// The wave stops streaming once no lane needs a later sample (converged pixels stop early).
-constexpr int kRecWave = 64, kRecChunk = 256, kRecLoads = 3 * kRecChunk / kRecWave;
-__global__ __launch_bounds__(kRecWave) void k_adapt_record(PixelSoA px, const double* __restrict__ L, int64_t nq,
-                                                           int64_t npix, AdaptPlan ap) {
-  __shared__ double st[3 * kRecChunk];
-  const int t = threadIdx.x;
-  const int64_t q0 = (int64_t)blockIdx.x * kRecWave, q = q0 + t;
-  const bool inq = q < nq;
+// One lane per sub-pixel: the replay of a pixel's samples is sequential (each step divides by
+// the running count), so the parallelism is across pixels, and each lane streams its own run
+// of the phase's slots with the loads of the next kRecAhead samples in flight while it
+// replays the current one (a lane's run is contiguous: its loads walk the same cache lines).
+constexpr int kRecAhead = 4;
+__global__ __launch_bounds__(kBlock) void k_adapt_record(PixelSoA px, const double* __restrict__ L, int64_t nq,
+                                                         int64_t npix, AdaptPlan ap) {
+  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (q == 0) *ap.active = 0;  // k_adapt_expand, later on the stream, counts the next phase's pixels
+  if (q >= nq) return;
   const int64_t p = q * ap.sub_n + ap.sub_j;
-  int K = 0;
-  int64_t o = 0;
-  if (inq) {
-    K = ap.kcur ? (int)ap.kcur[q] : ap.kuni;
-    o = ap.off ? (int64_t)ap.off[q] : p * (int64_t)ap.kuni;
-  }
-  bool live = inq && K > 0 && !px.conv[p];
-  double sum[3] = {0, 0, 0}, mean[3] = {0, 0, 0}, m2[3] = {0, 0, 0};
-  int n = 0;
-  bool conv = false;
-  if (live) {
+  const int K = ap.kcur ? (int)ap.kcur[q] : ap.kuni;
+  uint32_t kn = 0;
+  if (K > 0 && !px.conv[p]) {
+    const double* __restrict__ Lp = L + 3 * (ap.off ? (int64_t)ap.off[q] : p * (int64_t)ap.kuni);
+    double sum[3], mean[3], m2[3];
     for (int c = 0; c < 3; c++) sum[c] = px.sum[c * npix + p], mean[c] = px.mean[c * npix + p], m2[c] = px.m2[c * npix + p];
-    n = px.samples[p];
-  }
-  // the slots the wave's batches span (runs in q order; the uniform first phase interleaves
-  // the other sub-renders' pixels, which are loaded and skipped)
-  const int last = (int)min<int64_t>(kRecWave - 1, nq - 1 - q0);
-  const int64_t lo = __shfl(o, 0), hi = __shfl(o + K, last);
-  const double* __restrict__ src = L + 3 * lo;
-  const int64_t nd = 3 * (hi - lo);  // doubles in the range
-  double v[kRecLoads];
-  auto load = [&](int64_t d0) {
-#pragma unroll
-    for (int i = 0; i < kRecLoads; i++) {
-      const int64_t e = d0 + t + (int64_t)kRecWave * i;
-      if (e < nd) v[i] = src[e];
-    }
-  };
-  if (nd > 0) load(0);
-  for (int64_t c0 = lo; c0 < hi; c0 += kRecChunk) {
-#pragma unroll
-    for (int i = 0; i < kRecLoads; i++) st[t + kRecWave * i] = v[i];
-    __syncthreads();
-    const int64_t c1 = c0 + kRecChunk;
-    if (c1 < hi) load(3 * (c1 - lo));
-    if (live && !conv) {
-      const int64_t s1 = min<int64_t>(o + K, c1);
-      for (int64_t sl = max<int64_t>(o, c0); sl < s1 && !conv; sl++) {
-        // RecordSample (pixel_state.h:22-39), then IsConverged (pixel_state.h:54-72)
-        const double* x = st + 3 * (sl - c0);
-        n++;
-        for (int c = 0; c < 3; c++) {
-          double mu = mean[c];
-          double delta = x[c] - mu;
-          mu += delta / n;
-          double delta2 = x[c] - mu;
-          mean[c] = mu;
-          m2[c] += delta2 * delta;
+    int n = px.samples[p];
+    bool conv = false;
+    // RecordSample (pixel_state.h:22-39), then IsConverged (pixel_state.h:54-72)
+    auto record = [&](const double (&x)[3]) {
+      n++;
+      for (int c = 0; c < 3; c++) {
+        double mu = mean[c];
+        double delta = x[c] - mu;
+        mu += delta / n;
+        double delta2 = x[c] - mu;
+        mean[c] = mu;
+        m2[c] += delta2 * delta;
+      }
+      for (int c = 0; c < 3; c++) sum[c] += x[c];
+      if (n >= ap.min_spp) {
+        bool ok = true;
+        for (int c = 0; c < 3 && ok; c++) {
+          double var = n > 1 ? m2[c] / (n - 1) : 0.0;
+          double mu = fmax(fabs(mean[c]), 1e-3);
+          double err = sqrt(var) / sqrt((double)n);
+          if (err / mu > ap.rel) ok = false;
         }
-        for (int c = 0; c < 3; c++) sum[c] += x[c];
-        if (n >= ap.min_spp) {
-          bool ok = true;
-          for (int c = 0; c < 3 && ok; c++) {
-            double var = n > 1 ? m2[c] / (n - 1) : 0.0;
-            double mu = fmax(fabs(mean[c]), 1e-3);
-            double err = sqrt(var) / sqrt((double)n);
-            if (err / mu > ap.rel) ok = false;
-          }
-          conv = ok;
-        }
+        conv = ok;
+      }
+    };
+    double b[kRecAhead][3];
+    auto load = [&](int slot, int k) {
+      if (k < K)
+        for (int c = 0; c < 3; c++) b[slot][c] = Lp[3 * k + c];
+    };
+#pragma unroll
+    for (int i = 0; i < kRecAhead; i++) load(i, i);
+    for (int k = 0; k < K && !conv; k += kRecAhead) {
+#pragma unroll
+      for (int i = 0; i < kRecAhead; i++) {
+        if (k + i >= K || conv) break;
+        record(b[i]);
+        load(i, k + i + kRecAhead);
       }
     }
-    __syncthreads();
-    if (__ballot(live && !conv && o + K > c1) == 0) break;  // no lane needs a later slot
-  }
-  if (!inq) return;
-  uint32_t kn = 0;
-  if (live) {
     for (int c = 0; c < 3; c++) px.sum[c * npix + p] = sum[c], px.mean[c * npix + p] = mean[c], px.m2[c * npix + p] = m2[c];
     px.samples[p] = n;
     px.conv[p] = conv;
@@ -711,15 +701,19 @@ __global__ __launch_bounds__(kBlock) void k_adapt_expand(const uint32_t* __restr
   const int t = threadIdx.x;
   const int64_t q0 = (int64_t)blockIdx.x * kBlock, q = q0 + t;
   const int nb = (int)min<int64_t>(kBlock, nq - q0);
+  bool act = false;
   if (t < nb) {
     const uint32_t k = knext[q], o = off[q];
     const int64_t p = q * sub_n + sub_j;
+    act = k != 0;
     s_off[t] = o, s_p[t] = (uint32_t)p, s_s0[t] = k ? (uint32_t)samples[p] : 0u;
     if (t == nb - 1) {
       s_end = o + k;
-      if (q == nq - 1) *total = (unsigned long long)o + k;
+      if (q == nq - 1) total[0] = (unsigned long long)o + k, total[2] = (unsigned long long)smap;
     }
   }
+  const unsigned long long nact = __popcll(__ballot(act));  // total[1]: the phase's pixels
+  if (nact && lane_id() == 0) atomicAdd(total + 1, nact);
   __syncthreads();
   const uint32_t b = s_off[0], e = s_end;
   for (uint32_t i = b + t; i < e; i += kBlock) {

@@ -1,5 +1,5 @@
 // PARK instantiations of the persistent kernel (k_persistent<STACK, true, COUNT, SCATTER,
-// true>), compiled apart from rtx_capi.hip so this translation unit can have its own macro
+// PARK = 1 or 2>), compiled apart from rtx_capi.hip so this translation unit can have its own macro
 // defaults (below) and scheduler options (see the Makefile and rtx_kernels.h).
 #define RTX_PERSISTENT_ONLY 1
 // the library cos()/sin() here: with the small-argument form the bunny's triangle-tree
@@ -28,16 +28,17 @@
 #include "rtx_kernels.h"
 
 namespace rtxd {
-#define RTX_PARK_DEFINE(ST, CO, SC) \
-  template __global__ void k_persistent<ST, true, CO, SC, true>(RenderArgs, unsigned long long*);
+#define RTX_PARK_DEFINE(ST, CO, SC, MP, PK)                                                                     \
+  template __global__ void k_persistent<ST, true, CO, SC, PK, -1, false, false, false, MP>(RenderArgs,          \
+                                                                                          unsigned long long*);
 RTX_PARK_INSTANCES(RTX_PARK_DEFINE)
 #undef RTX_PARK_DEFINE
-#define RTX_PARK_TRI_DEFINE(ST)                                                                              \
-  template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE, false>(RenderArgs,     \
-                                                                                              unsigned long long*); \
-  template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE, true>(RenderArgs,      \
-                                                                                             unsigned long long*); \
-  template __global__ void k_persistent<ST, true, false, false, true, RTX_PRIM_TRIANGLE, true, true>(             \
+#define RTX_PARK_TRI_DEFINE(ST, MP, PK)                                                                              \
+  template __global__ void k_persistent<ST, true, false, false, PK, RTX_PRIM_TRIANGLE, false, false, false, MP>(    \
+      RenderArgs, unsigned long long*);                                                                              \
+  template __global__ void k_persistent<ST, true, false, false, PK, RTX_PRIM_TRIANGLE, true, false, false, MP>(     \
+      RenderArgs, unsigned long long*);                                                                              \
+  template __global__ void k_persistent<ST, true, false, false, PK, RTX_PRIM_TRIANGLE, true, true, false, MP>(      \
       RenderArgs, unsigned long long*);
 RTX_PARK_TRI_INSTANCES(RTX_PARK_TRI_DEFINE)
 #undef RTX_PARK_TRI_DEFINE

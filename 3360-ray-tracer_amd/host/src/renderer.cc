@@ -78,17 +78,13 @@ WavefrontRenderer::~WavefrontRenderer() {
 
 void WavefrontRenderer::set_devices(const std::vector<int>& devices, int stripe_rows) {
   // devices[0] renders through the integrator's own scene: it must be the integrator's device
-  // (a list without it would leave a listed device unused), and no device may appear twice
+  // (a list without it would leave a listed device unused).  A device may appear more than
+  // once: each entry gets its own scene copy, thread and stream (rtx_render_multi).
   auto* gpu = dynamic_cast<integrator::GpuRayIntegrator*>(&integrator);
   const int own = gpu ? gpu->device() : 0;
   if (!devices.empty() && devices[0] != own)
     throw std::invalid_argument("WavefrontRenderer::set_devices: the first device must be the integrator's (device " +
                                 std::to_string(own) + ")");
-  for (size_t a = 0; a < devices.size(); a++)
-    for (size_t b = a + 1; b < devices.size(); b++)
-      if (devices[a] == devices[b])
-        throw std::invalid_argument("WavefrontRenderer::set_devices: device " + std::to_string(devices[a]) +
-                                    " listed twice");
   for (rtx_scene* s : extra_) rtx_scene_destroy(s);
   extra_.clear();
   devices_ = devices;

@@ -18,10 +18,13 @@ RTX_OK = 0
 RTX_SEAM_TMIN = float(np.float32(0.001))
 MODES = {"wavefront": 0, "persistent": 1, "megakernel": 2}
 PRECISIONS = {"parity": 0, "fast": 1}
-RTX_FLAG_COUNT, RTX_FLAG_PARK, RTX_FLAG_NO_PARK, RTX_FLAG_GENERIC = 1, 2, 4, 8
-SCHEDULE_FLAGS = {None: 0, "auto": 0, "park": RTX_FLAG_PARK, "plain": RTX_FLAG_NO_PARK}
+RTX_FLAG_COUNT, RTX_FLAG_PARK, RTX_FLAG_NO_PARK, RTX_FLAG_GENERIC, RTX_FLAG_LEAF_STEP = 1, 2, 4, 8, 16
+# "park": the PARK schedule with its default walk (speculative on trees of at most 65536 nodes);
+# "park_step": the PARK schedule with the leaf-step walk on every tree
+SCHEDULE_FLAGS = {None: 0, "auto": 0, "park": RTX_FLAG_PARK, "park_step": RTX_FLAG_PARK | RTX_FLAG_LEAF_STEP,
+                  "plain": RTX_FLAG_NO_PARK}
 BUILD_BITS = {"park": 1, "sphere_tree": 2, "triangle_tree": 4, "lambertian": 8, "no_textures": 16,
-              "no_defocus": 32, "fast": 64, "count": 128, "scatter": 256}
+              "no_defocus": 32, "fast": 64, "count": 128, "scatter": 256, "speculative": 512}
 
 
 def build_names(bits):

@@ -118,7 +118,7 @@ def main():
     ap.add_argument("--mode", default="persistent", choices=["wavefront", "persistent"])
     ap.add_argument("--precision", default="fast", choices=["parity", "fast"])
     ap.add_argument("--seed", type=int, default=1234)
-    ap.add_argument("--schedule", default="auto", choices=["auto", "plain", "park"],
+    ap.add_argument("--schedule", default="auto", choices=["auto", "plain", "park", "park_step"],
                     help="persistent fast schedule: auto = timed per scene by the library (default); "
                          "plain/park force one (identical results; used by scripts/profile.sh so the "
                          "trace holds no schedule-timing launches)")
@@ -295,7 +295,8 @@ def main():
                                    + (f", one frame split over {world} GPUs" if world > 1 else ""),
                        "scene_prims": int(host.desc().n_prims), "bvh_nodes": int(host.desc().n_nodes),
                        "mode": args.mode, "precision": args.precision,
-                       "schedule": "park" if parked else "plain", "kernel_build": rtx.build_names(build_bits),
+                       "schedule": ("park_step" if args.schedule == "park_step" else "park") if parked else "plain",
+                       "kernel_build": rtx.build_names(build_bits),
                        "timed_region": "first ray generation -> framebuffer on the host (D2H inside each step)",
                        "framebuffer": "pinned host" if frame.pinned else "pageable host (pinned staging)",
                        "frame_rows_covered": covered,
@@ -377,7 +378,7 @@ def cpu_baseline(rtx, dev, host, cam, preset, scene_name, spp, depth, args, park
         t0 = time.perf_counter()
         ref, ref_spp, st = s.render(cfg, W, spp, depth, args.seed, tile=tile, **ad)
         dt = time.perf_counter() - t0
-    sched = "park" if parked else "plain"
+    sched = ("park_step" if args.schedule == "park_step" else "park") if parked else "plain"
     gpu, gpu_spp, gst = dev.render(cam, spp, depth, seed=args.seed, adaptive=args.adaptive, tile=tile, mode=args.mode,
                                    precision=args.precision, schedule=sched if args.mode == "persistent" else None,
                                    generic=args.generic, min_spp=ADAPTIVE_MIN_SPP, rel_threshold=ADAPTIVE_REL)

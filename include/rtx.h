@@ -41,8 +41,9 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 4  /* 2: rtx_stats.node_bytes; 3: rtx_stats.parked, RTX_FLAG_PARK / NO_PARK;
-                              4: rtx_stats.build, RTX_FLAG_GENERIC, rtx_render_multi */
+#define RTX_ABI_VERSION 5  /* 2: rtx_stats.node_bytes; 3: rtx_stats.parked, RTX_FLAG_PARK / NO_PARK;
+                              4: rtx_stats.build, RTX_FLAG_GENERIC, rtx_render_multi;
+                              5: RTX_FLAG_LEAF_STEP, RTX_BUILD_SPECULATIVE */
 
 enum {
   RTX_OK = 0,
@@ -203,7 +204,11 @@ enum {
   RTX_FLAG_NO_PARK = 4, /* every traversal runs to completion within its round */
   /* RTX_MODE_PERSISTENT: run the generic kernel build, without the per-scene
      specialisations (same results; for measuring what the specialisations buy) */
-  RTX_FLAG_GENERIC = 8
+  RTX_FLAG_GENERIC = 8,
+  /* the PARK schedule's traversal: the speculative walk (queued leaf tests) by default on
+     trees of at most 65536 BVH4 nodes, the leaf-step walk on larger ones; this flag asks for
+     the leaf-step walk on every tree (same results) */
+  RTX_FLAG_LEAF_STEP = 16
 };
 
 /* rtx_stats.build: which persistent-kernel build ran (the per-scene specialisations compile
@@ -217,7 +222,8 @@ enum {
   RTX_BUILD_NO_DEFOCUS = 32,    /* no thin-lens camera sampling (defocus_angle <= 0) */
   RTX_BUILD_FAST = 64,          /* RTX_PREC_FAST traversal */
   RTX_BUILD_COUNT = 128,        /* diagnostic counting build */
-  RTX_BUILD_SCATTER = 256       /* MegaKernel (Scatter API) semantics */
+  RTX_BUILD_SCATTER = 256,      /* MegaKernel (Scatter API) semantics */
+  RTX_BUILD_SPECULATIVE = 512   /* PARK schedule with the speculative walk (else the leaf-step walk) */
 };
 
 typedef struct {

@@ -27,6 +27,7 @@ CASES = [  # scene recipe, camera preset, width, spp, depth, mode, precision, ad
     ("bunny", "c3_bunny", 160, 16, 20, "persistent", "fast", False, "park"),  # the PARK kernel, forced
     ("mixed", "c5_mixed", 96, 8, 50, "persistent", "fast", False, "park"),
     ("cornell", "cornell", 64, 16, 50, "persistent", "fast", False, "park"),
+    ("bunny", "c3_bunny", 160, 16, 20, "persistent", "fast", False, "park_step"),  # PARK, leaf-step walk
     ("bunny", "c3_bunny", 400, 64, 20, "persistent", "fast", True),  # adaptive, two sub-renders
     ("final", "c2_final", 400, 48, 50, "persistent", "fast", True),
 ]

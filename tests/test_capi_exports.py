@@ -29,7 +29,7 @@ def test_every_declared_symbol_is_exported(rtx_mod):
 
 
 def test_abi_version(rtx_mod):
-    assert rtx_mod.lib().rtx_abi_version() == 4
+    assert rtx_mod.lib().rtx_abi_version() == 5
 
 
 def test_library_is_a_gfx950_code_object(rtx_mod):
@@ -59,7 +59,7 @@ def test_invalid_descriptors_rejected_before_launch(rtx_mod):
     assert rc == -1 and b"material out of range" in rtx_mod.lib().rtx_last_error()
 
 
-@pytest.mark.parametrize("park", [0, 1])
+@pytest.mark.parametrize("park", [0, 1, 2])
 def test_persistent_lds_regions_are_disjoint(rtx_mod, park):
     """The persistent kernel's LDS regions (traversal stacks, throughput, hit point, leaf queue)
     are each lane-interleaved with their own element size, so a byte shared by two regions
@@ -74,6 +74,7 @@ def test_persistent_lds_regions_are_disjoint(rtx_mod, park):
     for slots in range(1, 66):
         assert f(slots, park, out) == 0
         stack, thr, hitp, leafq, end, *per_lane = list(out)
+        assert (per_lane[3] != 0) == (park == 2) and per_lane[0] == slots * (2 if park == 2 else 4)
         regions = [(o, o + 256 * b) for o, b in zip((stack, thr, hitp, leafq), per_lane) if b]
         regions.sort()
         assert regions[0][0] == 0 and regions[-1][1] == end, (slots, regions, end)

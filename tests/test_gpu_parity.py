@@ -343,14 +343,43 @@ def test_parked_traversal_schedule_is_bit_identical(rtx_mod, dev_scenes, scene, 
     cam = rtx_mod.camera(rtx_mod.camera_config(preset, width=w))
     d = dev_scenes(scene)
     out = {}
-    for sched in ("plain", "park", None):
+    for sched in ("plain", "park", "park_step", None):
         out[sched] = d.render(cam, spp, depth, seed=5, adaptive=adaptive, mode="persistent", precision="fast",
                               schedule=sched)
     (a, sa, sta), (b, sb, stb), (c, sc, stc) = out["plain"], out["park"], out[None]
+    e, se, ste = out["park_step"]
     fast4 = stb["node_bytes"] == 128  # the BVH4 fast path exists (a flat list renders in parity precision)
     assert sta["parked"] == 0 and stb["parked"] == (1 if fast4 else 0) and stc["parked"] in (0, 1)
+    # small trees: the PARK schedule walks speculatively unless the leaf-step walk is asked for
+    assert ("speculative" in rtx_mod.build_names(stb["build"])) == fast4
+    assert "speculative" not in rtx_mod.build_names(ste["build"]) and ste["parked"] == stb["parked"]
     assert np.array_equal(a, b) and np.array_equal(sa, sb) and sta["rays_total"] == stb["rays_total"]
+    assert np.array_equal(a, e) and np.array_equal(sa, se) and sta["rays_total"] == ste["rays_total"]
     assert np.array_equal(a, c) and np.array_equal(sa, sc)
+
+
+def test_park_schedule_on_a_tree_above_the_speculative_limit(rtx_mod, tmp_path):
+    """The speculative walk keeps 16-bit node indices on its traversal stack, so trees of more
+    than 65536 BVH4 nodes run the PARK schedule with the leaf-step walk (the host picks it;
+    RTX_FLAG_PARK is honoured, not refused): same pixels, sample and segment counts as the
+    plain kernel."""
+    rng = np.random.default_rng(21)
+    n = 500_000
+    c = rng.uniform(-30, 30, (n, 3))
+    c[:, 1] = rng.uniform(0.05, 8, n)
+    r = rng.uniform(0.01, 0.05, n)
+    lines = ["rtxscene 1", "bvh 1", "tex 0 solid 0.6 0.5 0.4", "mat 0 lambertian 0", "sphere 0 -1000 0 1000 0"]
+    lines += ["sphere %.6f %.6f %.6f %.6f 0" % (x, y, z, rr) for (x, y, z), rr in zip(c, r)]
+    p = tmp_path / "many_spheres.rtxs"
+    p.write_text("\n".join(lines) + "\n")
+    d = rtx_mod.DeviceScene(rtx_mod.HostScene.load(str(p)))
+    cam = rtx_mod.camera(rtx_mod.camera_config("c2_final", width=48))
+    a, sa, sta = d.render(cam, 4, 8, seed=9, adaptive=False, mode="persistent", precision="fast", schedule="plain")
+    b, sb, stb = d.render(cam, 4, 8, seed=9, adaptive=False, mode="persistent", precision="fast", schedule="park")
+    assert stb["node_bytes"] == 128 and stb["parked"] == 1
+    names = rtx_mod.build_names(stb["build"])
+    assert "park" in names and "speculative" not in names, names
+    assert np.array_equal(a, b) and np.array_equal(sa, sb) and sta["rays_total"] == stb["rays_total"]
 
 
 # A Cornell box with earthmap on its walls, an earthmap-textured emitter, an image-textured

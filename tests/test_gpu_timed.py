@@ -59,10 +59,20 @@ BENCH_CASES = [
     ("bunny", "c4_bunny4k", 3840, 4, 50, set(), TRI),
     ("mixed", "c5_mixed", 3840, 4, 50, {"sphere_tree"}, {"park"}),
 ]
-SPECIALISED = {"sphere_tree", "triangle_tree", "lambertian", "no_textures", "no_defocus", "park"}
+SPECIALISED = {"sphere_tree", "triangle_tree", "lambertian", "no_textures", "no_defocus", "park", "speculative"}
 
 
-@pytest.mark.parametrize("schedule", ["plain", "park", "auto"])
+def want_build(schedule, st, plain_build, park_build):
+    """The build a schedule runs: the PARK one walks speculatively on these trees (all under
+    65536 BVH4 nodes) unless the leaf-step walk is asked for."""
+    if schedule == "park_step":
+        return park_build
+    if schedule == "plain" or (schedule == "auto" and not st["parked"]):
+        return plain_build
+    return park_build | {"speculative"}
+
+
+@pytest.mark.parametrize("schedule", ["plain", "park", "park_step", "auto"])
 @pytest.mark.parametrize("case", BENCH_CASES, ids=[c[1] for c in BENCH_CASES])
 def test_timed_kernel_builds_match_oracle(rtx_mod, orc, scenes, case, schedule):
     scene, preset, width, spp, depth, plain_build, park_build = case
@@ -73,7 +83,7 @@ def test_timed_kernel_builds_match_oracle(rtx_mod, orc, scenes, case, schedule):
     rgb, sp, st = d.render(cam, spp, depth, seed=77, adaptive=False, mode="persistent", precision="fast", tile=tile,
                            schedule=schedule)
     names = set(rtx_mod.build_names(st["build"])) & SPECIALISED
-    want = {"plain": plain_build, "park": park_build}.get(schedule) or (park_build if st["parked"] else plain_build)
+    want = want_build(schedule, st, plain_build, park_build)
     assert names == want, (names, want)
     rms = np.sqrt(np.mean((rgb - ref.reshape(-1, 3)) ** 2))
     assert rms <= RMS_TOL, rms
@@ -94,7 +104,7 @@ ADAPTIVE_CASES = [  # bench case index, spp, band rows
 ADAPTIVE_MIN, ADAPTIVE_REL = 16, float(np.float32(0.05))
 
 
-@pytest.mark.parametrize("schedule", ["plain", "park", "auto"])
+@pytest.mark.parametrize("schedule", ["plain", "park", "park_step", "auto"])
 @pytest.mark.parametrize("acase", ADAPTIVE_CASES, ids=[BENCH_CASES[c[0]][1] for c in ADAPTIVE_CASES])
 def test_timed_kernel_builds_adaptive_match_oracle(rtx_mod, orc, scenes, acase, schedule):
     """Per-pixel sample counts equal the oracle's exactly, pixels within RMS_TOL: whatever
@@ -108,7 +118,7 @@ def test_timed_kernel_builds_adaptive_match_oracle(rtx_mod, orc, scenes, acase, 
     rgb, sp, st = d.render(cam, spp, depth, seed=515, adaptive=True, mode="persistent", precision="fast", tile=tile,
                            schedule=schedule, min_spp=ADAPTIVE_MIN, rel_threshold=ADAPTIVE_REL)
     names = set(rtx_mod.build_names(st["build"])) & SPECIALISED
-    want = {"plain": plain_build, "park": park_build}.get(schedule) or (park_build if st["parked"] else plain_build)
+    want = want_build(schedule, st, plain_build, park_build)
     assert names == want, (names, want)
     ref_spp = ref_spp.ravel()
     assert np.array_equal(sp, ref_spp), (np.nonzero(sp != ref_spp)[0][:5], sp[sp != ref_spp][:5])
@@ -128,7 +138,7 @@ def test_generic_build_equals_specialised(rtx_mod, scenes, case):
     a, sa, sta = d.render(cam, spp, depth, seed=3, adaptive=False, mode="persistent", precision="fast", tile=tile)
     b, sb, stb = d.render(cam, spp, depth, seed=3, adaptive=False, mode="persistent", precision="fast", tile=tile,
                           generic=True)
-    spec = set(rtx_mod.build_names(stb["build"])) & (SPECIALISED - {"park"})
+    spec = set(rtx_mod.build_names(stb["build"])) & (SPECIALISED - {"park", "speculative"})
     assert not spec, spec
     assert sta["parked"] == stb["parked"]  # the generic flag keeps the scene's schedule
     assert np.array_equal(a, b) and np.array_equal(sa, sb) and sta["rays_total"] == stb["rays_total"]
