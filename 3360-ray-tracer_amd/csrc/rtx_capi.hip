@@ -735,8 +735,14 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ap.kmin = (int32_t)std::min<int64_t>(budget, (kAdaptPhaseSlots + active - 1) / std::max<int64_t>(1, active));
     ap.rel = prm->rel_threshold;
     ap.active = w.ctr.as<unsigned long long>() + 8 * 16 + 1;
-    hipLaunchKernelGGL(k_adapt_record, dim3((unsigned)((nq[j] + kBlock - 1) / kBlock)), dim3(kBlock), 0, st, px, Lph,
-                       nq[j], npix, ap);
+    ap.next_active = w.ctr.as<unsigned long long>() + 8 * 16 + 3;
+    HIPC(hipMemsetAsync(ap.next_active, 0, sizeof(unsigned long long), st));
+    const unsigned qb = (unsigned)((nq[j] + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_adapt_record, dim3(qb), dim3(kBlock), 0, st, px, Lph, nq[j], npix, ap);
+    HIPC(hipGetLastError());
+    hipLaunchKernelGGL(k_adapt_floor, dim3(qb), dim3(kBlock), 0, st, ap.knext, nq[j], S, j,
+                       (const int32_t*)px.samples, budget, kcap[j], (int64_t)kAdaptPhaseSlots / S,
+                       (const unsigned long long*)ap.next_active);
     HIPC(hipGetLastError());
     int rc2;
     if ((rc2 = plan(j, st, ap.knext))) return rc2;

@@ -605,6 +605,7 @@ struct AdaptPlan {
   int32_t kmin;  // smallest next batch: keeps a phase with few pixels left large enough to fill the GPU
   double rel;
   unsigned long long* active;  // the next phase's pixel count (k_adapt_expand adds; zeroed here)
+  unsigned long long* next_active;  // ... counted here too (zeroed before the launch), for k_adapt_floor
 };
 __device__ __forceinline__ uint32_t adapt_next_batch(const double (&mean)[3], const double (&m2)[3], int n,
                                                      const AdaptPlan& ap) {
@@ -685,6 +686,27 @@ __global__ __launch_bounds__(kBlock) void k_adapt_record(PixelSoA px, const doub
     if (!conv && n < ap.budget) kn = adapt_next_batch(mean, m2, n, ap);
   }
   ap.knext[q] = kn;
+  const unsigned long long na = __popcll(__ballot(kn != 0));
+  if (na && lane_id() == 0) atomicAdd(ap.next_active, na);
+}
+// Once the next phase's pixel count is known: every batch at least target / that count (within
+// the pixel's budget and the workspace), so a phase with few pixels left is large enough to
+// fill the GPU, and the pixels finish in it rather than in further phases that would be mostly
+// launch drain (the last paths of a launch run with their waves nearly empty).
+__global__ __launch_bounds__(kBlock) void k_adapt_floor(uint32_t* __restrict__ knext, int64_t nq, int32_t sub_n,
+                                                        int32_t sub_j, const int32_t* __restrict__ samples,
+                                                        int32_t budget, int32_t kcap, int64_t target,
+                                                        const unsigned long long* __restrict__ next_active) {
+  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (q >= nq) return;
+  const uint32_t k = knext[q];
+  if (k == 0) return;
+  const unsigned long long na = *next_active;
+  const int64_t kmin = (target + (int64_t)na - 1) / (int64_t)max(na, 1ull);
+  const int left = budget - samples[q * sub_n + sub_j];
+  int kn = (int)max<int64_t>((int64_t)k, min<int64_t>(kmin, (int64_t)left));
+  kn = (kn + 3) & ~3;
+  knext[q] = (uint32_t)min(kn, min(left, kcap));
 }
 // The next phase's slot map: sub-pixel q's batch occupies slots [off[q], off[q] + knext[q]),
 // slot off[q] + k being sample samples[p] + k of pixel p.  One block per 256 sub-pixels; its

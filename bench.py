@@ -389,7 +389,11 @@ def cpu_baseline(rtx, dev, host, cam, preset, scene_name, spp, depth, args, park
             "sample": f"{what} {W}x{H} frame, {spp} spp, depth {depth}, fixed spp, "
                       f"{st['rays']} segments in {dt:.1f}s (oracle/rtx_oracle.cc, OpenMP on {threads} threads, philox)"
                       .replace("fixed spp", sampling_text(args.adaptive))}
-    cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+    # the calibration measured with this many threads (scripts/calibrate_cpu.py --threads N on
+    # the GPU box's host, profiles/cpu_calibration_<N>t.json) when there is one
+    cal = os.path.join(ROOT, "profiles", f"cpu_calibration_{threads}t.json")
+    if not os.path.exists(cal):
+        cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
     if os.path.exists(cal):
         c = json.load(open(cal))
         case = c["cases"].get(CALIBRATION_CASE.get(scene_name, ""))

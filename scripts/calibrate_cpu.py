@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""scripts/calibrate_cpu.py — TEST INFRASTRUCTURE (build container only; needs /root/reference).
+"""scripts/calibrate_cpu.py — TEST INFRASTRUCTURE (needs oracle/_ref/ref_harness, built in the build
+container from the reference's sources by oracle/Makefile; it travels to the GPU box with the tree).
 
 Times the reference's own renderer (oracle/_ref/ref_harness: the reference's CPURayIntegrator,
 materials and PixelState driven by the Render() glue of wavefront.cc:40-242; its OpenMP
@@ -8,7 +9,10 @@ cpu_baseline (oracle/librtx_oracle.so, per-pixel Philox mode, OpenMP) on identic
 configurations and the same number of threads, fixed spp.  The ratio port/reference
 calibrates bench.py's cpu_baseline against the reference.
 
-Writes profiles/cpu_calibration.json.  Usage: python scripts/calibrate_cpu.py [--threads 8]
+Writes profiles/cpu_calibration.json, or --out.  Usage:
+    python scripts/calibrate_cpu.py [--threads 8] [--out F] [--host "text"]
+The models directory is the reference's when it is present, else the package's assets (the
+same stanford-bunny.obj), so the same harness can run on the GPU box's host cores.
 """
 import argparse
 import json
@@ -24,7 +28,8 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 sys.path.insert(0, os.path.join(ROOT, "3360-ray-tracer_amd"))
 
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
-MODELS = "/root/reference/models"
+MODELS = "/root/reference/models" if os.path.isdir("/root/reference/models") else \
+    os.path.join(ROOT, "3360-ray-tracer_amd", "assets")
 # name, scene, preset, width, spp, depth (fixed spp; C2-C5 at reduced spp, the rate is per segment)
 CASES = [
     ("c1_three", "three", "c1_three", 400, 4, 4),
@@ -38,12 +43,14 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
     ap.add_argument("--only", default="")
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "cpu_calibration.json"))
+    ap.add_argument("--host", default=f"build container, {os.cpu_count()} CPUs")
     args = ap.parse_args()
     import gen_golden
     import oracle_ctypes as orc
     import rtx
 
-    out = {"threads": args.threads, "host": f"build container, {os.cpu_count()} CPUs", "cases": {}}
+    out = {"threads": args.threads, "host": args.host, "cases": {}}
     with tempfile.TemporaryDirectory() as td:
         for name, scene, preset, width, spp, depth in CASES:
             if args.only and name not in args.only.split(","):
@@ -54,7 +61,7 @@ def main():
             env = dict(os.environ, REF_THREADS=str(args.threads))
             prefix = os.path.join(td, name)
             subprocess.run([str(a) for a in [HARNESS, "render", path, MODELS, *gen_golden.cam_args(cfg, width), depth, spp, 0, 1234,
-                            prefix]], check=True, env=env)
+                            prefix]], check=True, env=env, cwd=MODELS)  # (image textures by file name)
             st = dict(l.split() for l in open(prefix + ".stats"))
             ref_rays, ref_s = int(st["rays"]), float(st["loop_seconds"])
             s = orc.Scene(path)
@@ -71,7 +78,7 @@ def main():
                 "ratio_port_over_reference": port_rate / ref_rate,
             }
             print(name, json.dumps(out["cases"][name]), flush=True)
-    dst = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+    dst = args.out
     prev = json.load(open(dst)) if os.path.exists(dst) and args.only else {}
     if prev:
         prev["cases"].update(out["cases"])
