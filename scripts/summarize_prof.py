@@ -7,7 +7,12 @@
         FETCH_SIZE x 2 (gfx950 reports half of a wide coalesced read, MI355X_MICROARCH.md
         §HBM) + WRITE_SIZE, both in KiB units -> bytes, divided by the launch count.
 
-usage: summarize_prof.py gpurun_out/prof_<tag> <round> <workload> <mode> <precision>
+usage: summarize_prof.py gpurun_out/prof_<tag> <round> <workload> <mode> <precision> [adaptive]
+
+With `adaptive` (a bench --adaptive profile: phase launches of several instantiations), the
+VALU and HBM figures are the sums over every non-counting k_persistent launch divided by the
+segments of the profiled frames (warmup + steps frames of the PMC pass, identical frames), and
+the files are named ..._adaptive.json.
 """
 import collections
 import csv
@@ -22,6 +27,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     d, rnd, workload, mode, prec = sys.argv[1:6]
+    adaptive = len(sys.argv) > 6 and sys.argv[6] == "adaptive"
     tag = os.path.basename(d.rstrip("/")).replace("prof_", "")
     prof = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(prof, exist_ok=True)
@@ -42,6 +48,9 @@ def main():
         n = max(len(launches[(k, c)]) for c in v)
         out[k] = {"launches": n, **v}
     json.dump(out, open(os.path.join(prof, f"pmc_{tag}.json"), "w"), indent=1, sort_keys=True)
+    if adaptive:
+        adaptive_profile(d, out, rnd, tag, workload, mode, prec)
+        return
     # non-counting instantiation of the hot kernel (k_persistent<STACK, FAST, COUNT, SCATTER, PARK>:
     # either schedule; the one with the most wave cycles is the frame kernel)
     hot = "k_persistent<32, true, false, false," if mode == "persistent" else "k_wf_extend<32, true, false>"
@@ -107,6 +116,34 @@ def valu_profile(d, k, v, launches, hbm_per_launch, rnd, tag, workload, mode, pr
             out[c.lower() + "_per_launch"] = per_launch(v, launches, k, c)
     json.dump(out, open(os.path.join(ROOT, "profiles", f"valu_{workload}_{mode}_{prec}.json"), "w"), indent=1)
     print(json.dumps(out))
+
+
+def adaptive_profile(d, out, rnd, tag, workload, mode, prec):
+    """Sums over the frame kernels (non-counting k_persistent launches, every phase) per segment."""
+    ks = [k for k in out if k.startswith("void rtxd::k_persistent<") and ", true, false, false," in k]
+
+    def total(c):
+        return sum(out[k].get(c, 0.0) for k in ks)
+
+    def frames_segments(pass_glob):
+        b = glob.glob(os.path.join(d, pass_glob))
+        j = json.loads(open(b[0]).read().strip().splitlines()[-1])
+        return (j["warmup"] + j["steps"]) * j["rays_per_step"]
+
+    segs_valu = frames_segments("bench_pmc_SQ_INSTS_VALU*.json")
+    util = total("SQ_THREAD_CYCLES_VALU") / (64.0 * total("SQ_ACTIVE_INST_VALU"))
+    insts = total("SQ_INSTS_VALU")
+    hbm = None
+    if all(glob.glob(os.path.join(d, f"bench_pmc_{c}*.json")) for c in ("FETCH_SIZE", "WRITE_SIZE")):
+        hbm = (total("FETCH_SIZE") * 2 * 1024 / frames_segments("bench_pmc_FETCH_SIZE*.json")
+               + total("WRITE_SIZE") * 1024 / frames_segments("bench_pmc_WRITE_SIZE*.json"))
+    res = {"kernels": ks, "segments_profiled": segs_valu, "lane_utilisation": util,
+           "valu_insts_per_segment": insts / segs_valu, "lane_ops_per_segment": insts * 64 * util / segs_valu,
+           "hbm_bytes_per_segment": hbm, "source": f"profiles/{rnd}/pmc_{tag}.json",
+           "formula": "sums over every phase launch of the frame kernels / segments of the profiled frames"}
+    json.dump(res, open(os.path.join(ROOT, "profiles", f"valu_{workload}_{mode}_{prec}_adaptive.json"), "w"),
+              indent=1)
+    print(json.dumps(res))
 
 
 if __name__ == "__main__":
