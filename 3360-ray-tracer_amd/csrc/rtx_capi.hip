@@ -150,12 +150,12 @@ struct rtx_scene {
   hipStream_t copy_stream = nullptr;
   std::vector<hipEvent_t> band_ev;
   AdaptWs aw[kAdaptSubs];
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr, offset_ev = nullptr;
   double slot_mem = -1.0;  // bytes the slot buffers may take (slot_target; -1: not yet queried)
   ~rtx_scene() {
     (void)hipSetDevice(device);
     for (auto& w : aw) w.release();
-    for (hipEvent_t e : {fork_ev, join_ev})
+    for (hipEvent_t e : {fork_ev, join_ev, offset_ev})
       if (e) (void)hipEventDestroy(e);
     for (auto e : evpool) (void)hipEventDestroy(e);
     for (auto e : band_ev) (void)hipEventDestroy(e);
@@ -778,11 +778,14 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     }
   }
   if (S > 1) {  // the sub-renders' streams start once the first phase is done
-    for (hipEvent_t* e : {&sc->fork_ev, &sc->join_ev})
+    for (hipEvent_t* e : {&sc->fork_ev, &sc->join_ev, &sc->offset_ev})
       if (!*e) HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
     HIPC(hipEventRecord(sc->fork_ev, s));
     for (int j = 1; j < S; j++) HIPC(hipStreamWaitEvent(sc->aw[j].st, sc->fork_ev, 0));
   }
+  static const char* off_env = std::getenv("RTX_ADAPT_OFFSET");  // tuning: 0 = sub-renders in lockstep
+  const bool offset = S > 1 && !(off_env && std::atoi(off_env) == 0);
+  bool offset_recorded = false;
   bool alive[kAdaptSubs] = {false, false};
   for (int j = 0; j < S; j++) {
     if ((rc = record(j, j == 0 ? s : sc->aw[j].st, 1, sc->lbuf.as<double>(), nq[j]))) return rc;
@@ -810,6 +813,12 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
       Launch Lj = L;
       Lj.s = st;
       Lj.map = true;
+      // The sub-renders take turns: sub-render 1's second phase starts once sub-render 0's has
+      // ended, and from then on each phase's launch holds every CU slot it can get, so the
+      // other sub-render's record / scan / expand kernels and next phase find slots only as
+      // its last waves leave: each launch's drain is filled by the other sub-render's work.
+      // Queued together, the two phases would share the GPU and drain at the same time.
+      if (offset && j > 0 && g == 2 && offset_recorded) HIPC(hipStreamWaitEvent(st, sc->offset_ev, 0));
       HIPC(hipMemsetAsync(ctr, 0, 8 * 16 * sizeof(unsigned long long), st));
       unsigned long long seg0 = 0;
       if (debug) {
@@ -821,6 +830,10 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
       if ((rc = persist_m<false>(Lj, Aj, ctr))) return rc;
       if ((rc = mark(st))) return rc;
       hot_launches++;
+      if (offset && j == 0 && g == 2) {
+        HIPC(hipEventRecord(sc->offset_ev, st));
+        offset_recorded = true;
+      }
       if (debug) {
         HIPC(hipEventRecord(sc->ev[3], st));
         HIPC(hipEventSynchronize(sc->ev[3]));
