@@ -92,7 +92,7 @@ float round_up(double x) {
 
 }  // namespace
 
-constexpr int kCounterWords = 64 + 8 * 16;  // statistics, queue counts, slot counter(s)
+constexpr int kCounterWords = 64 + 8 * 16 + 8;  // statistics, queue counts, slot counter(s), [196] segment buffer (0)
 
 // Where a render's output goes once a band of it is final (fixed-spp renders): the
 // accumulate of the last sample group runs in kBands bands of the frame's pixels, and after
@@ -112,13 +112,15 @@ constexpr int kBands = 8;  // bands of the last accumulate and of the D2H copies
 // next phase's size) overlaps the other's tracing.
 constexpr int kAdaptSubs = 2;
 constexpr int64_t kAdaptPhaseSlots = 1 << 21;  // render_adaptive: smallest phase a sub-render plans while pixels remain
+constexpr double kAdaptMarginStep = 0.25;      // render_adaptive: batch margin 1 + step * (phase - 1)
 struct AdaptWs {
-  DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address
+  DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer
+  DevBuf segs;                                  // counting renders: each slot's path segments (u16)
   HostBuf total_h;                              // pinned copy of the next phase's slot count
   hipStream_t st = nullptr;                     // sub-render 0 runs on the caller's stream
   hipEvent_t ev = nullptr;                      // total_h written
   void release() {
-    for (DevBuf* b : {&lbuf, &smap, &k[0], &k[1], &off, &scan_tmp, &ctr}) b->release();
+    for (DevBuf* b : {&lbuf, &smap, &k[0], &k[1], &off, &scan_tmp, &ctr, &segs}) b->release();
     total_h.release();
     if (ev) (void)hipEventDestroy(ev);
     if (st) (void)hipStreamDestroy(st);
@@ -131,6 +133,7 @@ struct rtx_scene {
   hipStream_t stream = nullptr;
   int cus = 0;
   DevBuf nodes, prims, mats, texs, images, fnodes, tri_n;
+  DevBuf segs1;  // counting adaptive renders: the first phase's per-slot path segments (u16)
   std::vector<DevBuf> texels;
   DScene S{};
   int stack_parity = 32, stack_fast = 32;
@@ -150,12 +153,12 @@ struct rtx_scene {
   hipStream_t copy_stream = nullptr;
   std::vector<hipEvent_t> band_ev;
   AdaptWs aw[kAdaptSubs];
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr, offset_ev = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
   double slot_mem = -1.0;  // bytes the slot buffers may take (slot_target; -1: not yet queried)
   ~rtx_scene() {
     (void)hipSetDevice(device);
     for (auto& w : aw) w.release();
-    for (hipEvent_t e : {fork_ev, join_ev, offset_ev})
+    for (hipEvent_t e : {fork_ev, join_ev})
       if (e) (void)hipEventDestroy(e);
     for (auto e : evpool) (void)hipEventDestroy(e);
     for (auto e : band_ev) (void)hipEventDestroy(e);
@@ -680,6 +683,15 @@ int time_park_schedule(rtx_scene* sc, const rtx_camera* cam, const rtx_render_pa
 // works on one sub-render while the other sits between phases.  `mark` records a hot-kernel
 // timing event on a stream (before and after each persistent launch); hot_launches counts
 // them.  The caller resolves the pixels (k_resolve) once both sub-renders are done.
+// Counting renders: the persistent launch's slot counter block names the buffer its paths'
+// segment counts go to (k_persistent COUNT builds read word 8 * 16 + 4 of it).
+int set_segbuf(unsigned long long* ctr, uint16_t* segs, hipStream_t st) {
+  const unsigned long long v = (unsigned long long)(uintptr_t)segs;
+  uint32_t* w = (uint32_t*)(ctr + 8 * 16 + 4);  // (two 32-bit memsets: stream-ordered, no host staging)
+  HIPC(hipMemsetD32Async((hipDeviceptr_t)w, (int)(uint32_t)v, 1, st));
+  HIPC(hipMemsetD32Async((hipDeviceptr_t)(w + 1), (int)(uint32_t)(v >> 32), 1, st));
+  return RTX_OK;
+}
 template <class Mark>
 int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const rtx_render_params* prm,
                     const PixelSoA& px, int budget, hipStream_t s, Mark mark, uint64_t& hot_launches) {
@@ -688,6 +700,11 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   const int S = (npix >= (1 << 16) && !(subs_env && std::atoi(subs_env) == 1)) ? kAdaptSubs : 1;
   const int K1 = std::min(std::max(1, prm->min_spp), budget);
   static const bool debug = std::getenv("RTX_DEBUG_ADAPT") != nullptr;  // per-phase slot counts on stderr
+  // tuning (A/B only): the smallest phase (log2 slots) and the per-phase batch margin step
+  static const char* ps_env = std::getenv("RTX_ADAPT_PHASE_SLOTS_LOG2");
+  static const char* mg_env = std::getenv("RTX_ADAPT_MARGIN_STEP");
+  const int64_t phase_slots = ps_env ? (1ll << std::min(30, std::max(10, std::atoi(ps_env)))) : kAdaptPhaseSlots;
+  const double margin_step = mg_env ? std::max(0.0, std::atof(mg_env)) : kAdaptMarginStep;
   if ((int64_t)npix * K1 > 0xFFFFFFFFll) return fail(RTX_ERR_INVALID, "adaptive render: npix x min_spp above 2^32");
   // slots per sub-render after the first phase: 24 B of radiance + 8 B of slot map each
   const int64_t cap = std::min<int64_t>(0xFFFFFFFFll, slot_target(sc, S * 32, (1ll << kSlotTargetLog2) / S));
@@ -701,6 +718,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     kcap[j] = (int32_t)std::min<int64_t>(budget, std::max<int64_t>(4, (cap / nq[j]) & ~3ll));
     const int64_t slots = nq[j] * (int64_t)kcap[j];
     if ((rc = w.lbuf.reserve(slots * 3 * sizeof(double)))) return rc;
+    if (L.count && (rc = w.segs.reserve(slots * sizeof(uint16_t)))) return rc;
     if ((rc = w.smap.reserve(slots * sizeof(uint2)))) return rc;
     for (DevBuf* b : {&w.k[0], &w.k[1], &w.off})
       if ((rc = b->reserve(nq[j] * sizeof(uint32_t)))) return rc;
@@ -732,8 +750,11 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ap.min_spp = prm->min_spp, ap.budget = budget, ap.phase = g, ap.kcap = kcap[j];
     // a phase of at least ~kAdaptPhaseSlots slots while pixels remain: once few pixels are left,
     // their batches grow (up to the budget) instead of phases that are mostly launch tail
-    ap.kmin = (int32_t)std::min<int64_t>(budget, (kAdaptPhaseSlots + active - 1) / std::max<int64_t>(1, active));
+    ap.kmin = (int32_t)std::min<int64_t>(budget, (phase_slots + active - 1) / std::max<int64_t>(1, active));
     ap.rel = prm->rel_threshold;
+    ap.margin_step = margin_step;
+    ap.segs = !L.count ? nullptr : g == 1 ? sc->segs1.as<uint16_t>() : w.segs.as<uint16_t>();
+    ap.rec_segs = A.counters + 9;
     ap.active = w.ctr.as<unsigned long long>() + 8 * 16 + 1;
     ap.next_active = w.ctr.as<unsigned long long>() + 8 * 16 + 3;
     HIPC(hipMemsetAsync(ap.next_active, 0, sizeof(unsigned long long), st));
@@ -741,7 +762,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     hipLaunchKernelGGL(k_adapt_record, dim3(qb), dim3(kBlock), 0, st, px, Lph, nq[j], npix, ap);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_adapt_floor, dim3(qb), dim3(kBlock), 0, st, ap.knext, nq[j], S, j,
-                       (const int32_t*)px.samples, budget, kcap[j], (int64_t)kAdaptPhaseSlots / S,
+                       (const int32_t*)px.samples, budget, kcap[j], (int64_t)phase_slots / S,
                        (const unsigned long long*)ap.next_active);
     HIPC(hipGetLastError());
     int rc2;
@@ -755,6 +776,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   // scene's radiance buffer)
   {
     if ((rc = sc->lbuf.reserve((size_t)npix * K1 * 3 * sizeof(double)))) return rc;
+    if (L.count && (rc = sc->segs1.reserve((size_t)npix * K1 * sizeof(uint16_t)))) return rc;
     RenderArgs A1 = A;
     A1.L = sc->lbuf.as<double>();
     A1.conv = nullptr;
@@ -763,6 +785,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     HIPC(hipMemsetAsync(ctr, 0, 8 * 16 * sizeof(unsigned long long), s));
     if (debug) HIPC(hipEventRecord(sc->ev[2], s));
     if ((rc = mark(s))) return rc;
+    if (L.count && (rc = set_segbuf(ctr, sc->segs1.as<uint16_t>(), s))) return rc;
     if ((rc = persist_m<false>(L, A1, ctr))) return rc;
     if ((rc = mark(s))) return rc;
     hot_launches++;
@@ -778,14 +801,11 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     }
   }
   if (S > 1) {  // the sub-renders' streams start once the first phase is done
-    for (hipEvent_t* e : {&sc->fork_ev, &sc->join_ev, &sc->offset_ev})
+    for (hipEvent_t* e : {&sc->fork_ev, &sc->join_ev})
       if (!*e) HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
     HIPC(hipEventRecord(sc->fork_ev, s));
     for (int j = 1; j < S; j++) HIPC(hipStreamWaitEvent(sc->aw[j].st, sc->fork_ev, 0));
   }
-  static const char* off_env = std::getenv("RTX_ADAPT_OFFSET");  // tuning: 0 = sub-renders in lockstep
-  const bool offset = S > 1 && !(off_env && std::atoi(off_env) == 0);
-  bool offset_recorded = false;
   bool alive[kAdaptSubs] = {false, false};
   for (int j = 0; j < S; j++) {
     if ((rc = record(j, j == 0 ? s : sc->aw[j].st, 1, sc->lbuf.as<double>(), nq[j]))) return rc;
@@ -813,12 +833,6 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
       Launch Lj = L;
       Lj.s = st;
       Lj.map = true;
-      // The sub-renders take turns: sub-render 1's second phase starts once sub-render 0's has
-      // ended, and from then on each phase's launch holds every CU slot it can get, so the
-      // other sub-render's record / scan / expand kernels and next phase find slots only as
-      // its last waves leave: each launch's drain is filled by the other sub-render's work.
-      // Queued together, the two phases would share the GPU and drain at the same time.
-      if (offset && j > 0 && g == 2 && offset_recorded) HIPC(hipStreamWaitEvent(st, sc->offset_ev, 0));
       HIPC(hipMemsetAsync(ctr, 0, 8 * 16 * sizeof(unsigned long long), st));
       unsigned long long seg0 = 0;
       if (debug) {
@@ -827,13 +841,10 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
         HIPC(hipEventRecord(sc->ev[2], st));
       }
       if ((rc = mark(st))) return rc;
+      if (L.count && (rc = set_segbuf(ctr, w.segs.as<uint16_t>(), st))) return rc;
       if ((rc = persist_m<false>(Lj, Aj, ctr))) return rc;
       if ((rc = mark(st))) return rc;
       hot_launches++;
-      if (offset && j == 0 && g == 2) {
-        HIPC(hipEventRecord(sc->offset_ev, st));
-        offset_recorded = true;
-      }
       if (debug) {
         HIPC(hipEventRecord(sc->ev[3], st));
         HIPC(hipEventSynchronize(sc->ev[3]));
@@ -1415,7 +1426,7 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
       HIPC(hipEventElapsedTime(&hms, sc->evpool[e], sc->evpool[e + 1]));
       hot_ms += hms;
     }
-    unsigned long long h[8];
+    unsigned long long h[10];
     HIPC(hipMemcpy(h, cnt, sizeof h, hipMemcpyDeviceToHost));
     stats->rays_total = h[0];
     stats->parked = L.park ? 1 : 0;
@@ -1432,6 +1443,9 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     stats->sphere_tests = h[7];
     stats->build = prm->mode == RTX_MODE_WAVEFRONT ? 0 : L.build;
     stats->node_bytes = L.fast ? sizeof(F4Node) : sizeof(rtx_bvh_node);
+    // segments of the recorded samples: counted per slot by the counting build in adaptive
+    // phases (k_adapt_record); every sample is recorded at fixed spp; unknown otherwise
+    stats->rays_recorded = !L.count ? 0 : phased ? h[9] : (prm->adaptive ? 0 : h[0]);
   }
   return RTX_OK;
 }
@@ -1582,6 +1596,7 @@ int rtx_render_multi(rtx_scene* const* scenes, int32_t n, const rtx_camera* cam,
       a.hot_launches += st[k].hot_launches, a.node_visits += st[k].node_visits, a.prim_tests += st[k].prim_tests;
       a.wave_node_iters += st[k].wave_node_iters, a.wave_prim_iters += st[k].wave_prim_iters;
       a.tri_tests += st[k].tri_tests, a.sphere_tests += st[k].sphere_tests;
+      a.rays_recorded += st[k].rays_recorded;
       a.node_bytes = st[k].node_bytes, a.parked |= st[k].parked, a.build |= st[k].build;
     }
     *stats = a;

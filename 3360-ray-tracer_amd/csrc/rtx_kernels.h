@@ -335,6 +335,11 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   const double tmin = SCATTER ? 0.001 : (double)0.001f;
   Counters c{};
   uint32_t segs = 0, prims = 0;
+  // counting builds: the lane's path segments, stored per slot when the launch's slot counter
+  // block names a buffer for them (adaptive renders: the segments of the recorded samples)
+  uint32_t pseg = 0;
+  uint16_t* const segbuf = COUNT ? (uint16_t*)next_slot[8 * 16 + 4] : nullptr;
+  (void)pseg, (void)segbuf;
   uint64_t chunk_base = 0, chunk_left = 0;  // wave-uniform
   bool exhausted = false;                   // wave-uniform
   uint32_t region = blockIdx.x & 7;         // wave-uniform
@@ -409,6 +414,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
         P.depth = SCATTER ? A.max_depth : 0;
         has = true;
         prims++;
+        if (COUNT) pseg = 0;
       }
     }
     if (!__any(has)) {
@@ -447,6 +453,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
         best = trace<STACK, FAST, COUNT, TK>(A.S, P.o, P.d, tmin, kInf, stk, c, tb, bmat);
       }
       segs++;
+      if (COUNT) pseg++;
       Hit h;
       rtx_material m;
       if (best >= 0) finish_hit_at<false>(A.S, best, tb, P.o, P.d, h);
@@ -491,6 +498,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
     }
     if (!cont) {
       store_radiance(A, slot, L);
+      if (COUNT && segbuf) segbuf[slot] = (uint16_t)min(pseg, 65535u);
       has = false;
     }
   }
@@ -604,6 +612,9 @@ struct AdaptPlan {
   int32_t min_spp, budget, phase, kcap;
   int32_t kmin;  // smallest next batch: keeps a phase with few pixels left large enough to fill the GPU
   double rel;
+  double margin_step;  // the batch margin grows by this much per phase (1 + step * (phase - 1))
+  const uint16_t* segs;           // counting renders: segments of each slot's path (else nullptr)
+  unsigned long long* rec_segs;   // ... summed here over the samples the pixels record
   unsigned long long* active;  // the next phase's pixel count (k_adapt_expand adds; zeroed here)
   unsigned long long* next_active;  // ... counted here too (zeroed before the launch), for k_adapt_floor
 };
@@ -616,7 +627,7 @@ __device__ __forceinline__ uint32_t adapt_next_batch(const double (&mean)[3], co
     need = fmax(need, var / (ap.rel * ap.rel * mu * mu));
   }
   const int left = ap.budget - n;
-  const double margin = 1.0 + 0.25 * (double)(ap.phase - 1);
+  const double margin = 1.0 + ap.margin_step * (double)(ap.phase - 1);
   const double want = (need - (double)n) * margin;
   int k = (want < (double)left) ? (int)ceil(want) : left;  // NaN / inf: the whole budget
   k = max(k, min(max(4 << min(ap.phase - 1, 4), ap.kmin), left));  // at least 4, 8, ... 64 more, and kmin
@@ -679,6 +690,12 @@ __global__ __launch_bounds__(kBlock) void k_adapt_record(PixelSoA px, const doub
         record(b[i]);
         load(i, k + i + kRecAhead);
       }
+    }
+    if (ap.segs) {  // counting render: the segments of the samples recorded (the rest are discarded)
+      const uint16_t* sg = ap.segs + (ap.off ? (int64_t)ap.off[q] : p * (int64_t)ap.kuni);
+      unsigned long long t = 0;
+      for (int k = 0; k < n - px.samples[p]; k++) t += sg[k];
+      atomicAdd(ap.rec_segs, t);
     }
     for (int c = 0; c < 3; c++) px.sum[c * npix + p] = sum[c], px.mean[c * npix + p] = mean[c], px.m2[c * npix + p] = m2[c];
     px.samples[p] = n;

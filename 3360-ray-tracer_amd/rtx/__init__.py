@@ -104,7 +104,7 @@ class Stats(C.Structure):
                 ("node_visits", C.c_uint64), ("prim_tests", C.c_uint64),
                 ("node_bytes", C.c_uint64), ("wave_node_iters", C.c_uint64), ("wave_prim_iters", C.c_uint64),
                 ("tri_tests", C.c_uint64), ("sphere_tests", C.c_uint64), ("parked", C.c_uint64),
-                ("build", C.c_uint64)]
+                ("build", C.c_uint64), ("rays_recorded", C.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

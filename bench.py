@@ -235,6 +235,14 @@ def main():
     # counting pass (diagnostic kernel build): segments, node visits and SIMD efficiency
     cst = step(params(rtx.RTX_FLAG_COUNT | sched_flags))
     segs = max(1, cst["rays_total"])
+    # adaptive sampling traces some samples past a pixel's convergence and discards them: the
+    # metric counts the segments of the recorded samples only (the counting pass renders the same
+    # frame and counts them per slot; deterministic, so the timed frames recorded as many)
+    recorded = cst["rays_recorded"] * steps
+    if dist is not None:
+        r = torch.tensor([float(recorded)], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        recorded = float(r.item())
     nodes_per_seg = cst["node_visits"] / segs
     simd_nodes = cst["node_visits"] / (64.0 * cst["wave_node_iters"]) if cst["wave_node_iters"] else None
     simd_prims = cst["prim_tests"] / (64.0 * cst["wave_prim_iters"]) if cst["wave_prim_iters"] else None
@@ -279,7 +287,7 @@ def main():
         out = {
             "metric": "Mrays/s (primary+secondary) at fixed spp; RMS pixel error vs CPU ref",
             "sampling": sampling_text(args.adaptive),
-            "value": rays_all / elapsed / 1e6,
+            "value": (recorded if args.adaptive else rays_all) / elapsed / 1e6,
             "unit": "Mrays/s",
             "n_gpus": world,
             "steps": steps,
@@ -304,11 +312,21 @@ def main():
             "roofline": roofline,
             "rays_per_step": rays_all / steps,
         }
+        if args.adaptive:
+            out["value_note"] = ("adaptive: value counts the segments of the recorded samples "
+                                 "(rays_recorded, counting pass); traced_value adds the samples traced past "
+                                 "a pixel's convergence and discarded")
+            out["traced_value"] = rays_all / elapsed / 1e6
+            out["rays_recorded_per_step"] = recorded / steps
         if generic_leg:
             out["generic_build"] = generic_leg
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"], out["rms_vs_cpu"], out["rms_check"] = cpu_baseline(
                 rtx, dev, host, cam, preset, scene_name, spp, depth, args, parked, build_bits)
+            rc = out["rms_check"]
+            if args.adaptive and rc["rows"] == [0, H]:  # the CPU rendered the whole frame
+                rc["segments_gpu_recorded"] = int(cst["rays_recorded"])
+                rc["recorded_segments_identical"] = int(cst["rays_recorded"]) == rc["segments_cpu"]
     frame.close(rank, dist)
     if rank == 0:
         print(json.dumps(out), flush=True)

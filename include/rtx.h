@@ -41,9 +41,9 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 5  /* 2: rtx_stats.node_bytes; 3: rtx_stats.parked, RTX_FLAG_PARK / NO_PARK;
+#define RTX_ABI_VERSION 6  /* 2: rtx_stats.node_bytes; 3: rtx_stats.parked, RTX_FLAG_PARK / NO_PARK;
                               4: rtx_stats.build, RTX_FLAG_GENERIC, rtx_render_multi;
-                              5: RTX_FLAG_LEAF_STEP, RTX_BUILD_SPECULATIVE */
+                              5: RTX_FLAG_LEAF_STEP, RTX_BUILD_SPECULATIVE; 6: rtx_stats.rays_recorded */
 
 enum {
   RTX_OK = 0,
@@ -242,6 +242,9 @@ typedef struct {
   uint64_t sphere_tests;
   uint64_t parked;          /* 1: the persistent fast schedule that parks long traversals ran */
   uint64_t build;           /* RTX_BUILD_* bits of the persistent kernel build (0: wavefront mode) */
+  uint64_t rays_recorded;   /* with RTX_FLAG_COUNT: segments of the samples the pixels recorded (adaptive
+                               sampling traces some samples past a pixel's convergence and discards them;
+                               = rays_total otherwise); 0 without RTX_FLAG_COUNT */
 } rtx_stats;
 
 /* ---- entry points ------------------------------------------------------------------ */

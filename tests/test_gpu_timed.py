@@ -128,6 +128,29 @@ def test_timed_kernel_builds_adaptive_match_oracle(rtx_mod, orc, scenes, acase, 
     assert rms <= RMS_TOL, rms
 
 
+@pytest.mark.parametrize("rows", [2, 70])
+@pytest.mark.parametrize("acase", ADAPTIVE_CASES[:2], ids=[BENCH_CASES[c[0]][1] for c in ADAPTIVE_CASES[:2]])
+def test_adaptive_recorded_segments_equal_oracle(rtx_mod, orc, scenes, acase, rows):
+    """The counting build's rays_recorded (the segments of the samples the pixels record; the
+    adaptive bench line's value counts only these) equals the oracle's segment count exactly, and
+    the samples traced past convergence are the difference to rays_total.  70 full-width rows are
+    >= 2^16 pixels, so the render runs as two interleaved sub-renders."""
+    ci, spp, _ = acase
+    scene, preset, width, _, depth, _, _ = BENCH_CASES[ci]
+    path, d = scenes(scene)
+    cam = rtx_mod.camera(rtx_mod.camera_config(preset, width=width))
+    tile = (0, cam.image_height // 2 - rows // 2, cam.image_width, rows)
+    ref, ref_spp, ref_st = oracle(orc, path, preset, width, spp, depth, 515, tile, adaptive=1)
+    rgb, sp, st = d.render(cam, spp, depth, seed=515, adaptive=True, mode="persistent", precision="fast", tile=tile,
+                           count=True, min_spp=ADAPTIVE_MIN, rel_threshold=ADAPTIVE_REL)
+    assert np.array_equal(sp, ref_spp.ravel())
+    assert st["rays_recorded"] == ref_st["rays"], (st["rays_recorded"], ref_st["rays"], st["rays_total"])
+    assert st["rays_total"] >= st["rays_recorded"]
+    _, _, fst = d.render(cam, 4, depth, seed=515, adaptive=False, mode="persistent", precision="fast", tile=tile,
+                         count=True)
+    assert fst["rays_recorded"] == fst["rays_total"] > 0  # fixed spp: every sample is recorded
+
+
 @pytest.mark.parametrize("case", BENCH_CASES, ids=[c[1] for c in BENCH_CASES])
 def test_generic_build_equals_specialised(rtx_mod, scenes, case):
     """Specialisation compiles out unreachable code only: identical pixels and counts."""
