@@ -106,25 +106,19 @@ struct BandSink {
 };
 constexpr int kBands = 8;  // bands of the last accumulate and of the D2H copies that overlap them (ab_bands_*: 2 / 4 / 8 / 16)
 
-// Adaptive renders in phases (render_adaptive): the pixels are split into kAdaptSubs
-// interleaved sub-renders, each with its own workspace and stream, so one sub-render's
-// phase-end work (the launch tail, the record / scan / expand kernels, the host's look at the
-// next phase's size) overlaps the other's tracing.
-constexpr int kAdaptSubs = 2;
-constexpr int64_t kAdaptPhaseSlots = 1 << 21;  // render_adaptive: smallest phase a sub-render plans while pixels remain
+// Adaptive renders in phases (render_adaptive)
+constexpr int64_t kAdaptPhaseSlots = 1 << 23;  // render_adaptive: smallest phase planned while pixels remain (ab r3x/r3y: 2^21..2^25)
 constexpr double kAdaptMarginStep = 0.25;      // render_adaptive: batch margin 1 + step * (phase - 1)
 struct AdaptWs {
   DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer
   DevBuf segs;                                  // counting renders: each slot's path segments (u16)
   HostBuf total_h;                              // pinned copy of the next phase's slot count
-  hipStream_t st = nullptr;                     // sub-render 0 runs on the caller's stream
   hipEvent_t ev = nullptr;                      // total_h written
   void release() {
     for (DevBuf* b : {&lbuf, &smap, &k[0], &k[1], &off, &scan_tmp, &ctr, &segs}) b->release();
     total_h.release();
     if (ev) (void)hipEventDestroy(ev);
-    if (st) (void)hipStreamDestroy(st);
-    ev = nullptr, st = nullptr;
+    ev = nullptr;
   }
 };
 
@@ -152,14 +146,11 @@ struct rtx_scene {
   // banded output copies (BandSink): a copy stream and its ordering events
   hipStream_t copy_stream = nullptr;
   std::vector<hipEvent_t> band_ev;
-  AdaptWs aw[kAdaptSubs];
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  AdaptWs aw;  // adaptive phases' workspace
   double slot_mem = -1.0;  // bytes the slot buffers may take (slot_target; -1: not yet queried)
   ~rtx_scene() {
     (void)hipSetDevice(device);
-    for (auto& w : aw) w.release();
-    for (hipEvent_t e : {fork_ev, join_ev})
-      if (e) (void)hipEventDestroy(e);
+    aw.release();
     for (auto e : evpool) (void)hipEventDestroy(e);
     for (auto e : band_ev) (void)hipEventDestroy(e);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
@@ -493,7 +484,7 @@ int64_t slot_target(rtx_scene* sc, int64_t bytes_per_slot, int64_t want) {
       fr = (size_t)1 << 62;
     }
     double held = (double)sc->lbuf.n + (double)sc->queue[0].n + (double)sc->queue[1].n;
-    for (const AdaptWs& w : sc->aw) held += (double)w.lbuf.n + (double)w.smap.n;
+    held += (double)sc->aw.lbuf.n + (double)sc->aw.smap.n;
     sc->slot_mem = 0.5 * ((double)fr + held);
   }
   return std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)(sc->slot_mem / (double)bytes_per_slot)));
@@ -672,17 +663,6 @@ int persist_m(const Launch& L, const RenderArgs& A, unsigned long long* ns) {
 
 int time_park_schedule(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm, hipStream_t s);
 
-// Adaptive sampling in phases on the persistent kernel (rtx_kernels.h, "Adaptive sampling in
-// phases"): the reference's WavefrontRenderer::Render loop (wavefront.cc:57-225, always
-// adaptive) with the same per-pixel results.  The pixels are split into kAdaptSubs interleaved
-// sub-renders (pixel p = q * S + j) with their own workspace, the first on the caller's stream
-// `s`, the second on a stream of its own.  Each sub-render runs: phase 1, min_spp samples of
-// every pixel; then, after each phase, record + next batch sizes (k_adapt_record); before
-// each phase, prefix sum and slot map (k_adapt_expand); the host reads the next phase's
-// slot count (one pinned word) only once the other sub-render's phase is queued, so the GPU
-// works on one sub-render while the other sits between phases.  `mark` records a hot-kernel
-// timing event on a stream (before and after each persistent launch); hot_launches counts
-// them.  The caller resolves the pixels (k_resolve) once both sub-renders are done.
 // Counting renders: the persistent launch's slot counter block names the buffer its paths'
 // segment counts go to (k_persistent COUNT builds read word 8 * 16 + 4 of it).
 int set_segbuf(unsigned long long* ctr, uint16_t* segs, hipStream_t st) {
@@ -692,12 +672,20 @@ int set_segbuf(unsigned long long* ctr, uint16_t* segs, hipStream_t st) {
   HIPC(hipMemsetD32Async((hipDeviceptr_t)(w + 1), (int)(uint32_t)(v >> 32), 1, st));
   return RTX_OK;
 }
+// Adaptive sampling in phases on the persistent kernel (rtx_kernels.h, "Adaptive sampling in
+// phases"): the reference's WavefrontRenderer::Render loop (wavefront.cc:57-225, always
+// adaptive) with the same per-pixel results, on the caller's stream `s`: phase 1, min_spp
+// samples of every pixel; then, after each phase, record + next batch sizes (k_adapt_record,
+// k_adapt_floor); before each phase, prefix sum and slot map (k_adapt_expand); the host reads
+// the next phase's slot count (one pinned word) to launch it or stop.  `mark` records a
+// hot-kernel timing event (before and after each persistent launch); hot_launches counts them.
+// The caller resolves the pixels (k_resolve).  (Round 3 also ran the pixels as two interleaved
+// sub-renders on two streams, meant to fill one's phase ends with the other's tracing: one
+// sequence is faster, C3 14.9 vs 15.7 ms per frame, DESIGN.md.)
 template <class Mark>
 int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const rtx_render_params* prm,
                     const PixelSoA& px, int budget, hipStream_t s, Mark mark, uint64_t& hot_launches) {
   const int64_t npix = A.npix;
-  static const char* subs_env = std::getenv("RTX_ADAPT_SUBS");  // tuning: sub-render count (1 or 2)
-  const int S = (npix >= (1 << 16) && !(subs_env && std::atoi(subs_env) == 1)) ? kAdaptSubs : 1;
   const int K1 = std::min(std::max(1, prm->min_spp), budget);
   static const bool debug = std::getenv("RTX_DEBUG_ADAPT") != nullptr;  // per-phase slot counts on stderr
   // tuning (A/B only): the smallest phase (log2 slots) and the per-phase batch margin step
@@ -706,88 +694,73 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   const int64_t phase_slots = ps_env ? (1ll << std::min(30, std::max(10, std::atoi(ps_env)))) : kAdaptPhaseSlots;
   const double margin_step = mg_env ? std::max(0.0, std::atof(mg_env)) : kAdaptMarginStep;
   if ((int64_t)npix * K1 > 0xFFFFFFFFll) return fail(RTX_ERR_INVALID, "adaptive render: npix x min_spp above 2^32");
-  // slots per sub-render after the first phase: 24 B of radiance + 8 B of slot map each
-  const int64_t cap = std::min<int64_t>(0xFFFFFFFFll, slot_target(sc, S * 32, (1ll << kSlotTargetLog2) / S));
-  int64_t nq[kAdaptSubs];
-  int32_t kcap[kAdaptSubs];
+  // slots after the first phase: 24 B of radiance + 8 B of slot map each
+  const int64_t cap = std::min<int64_t>(0xFFFFFFFFll, slot_target(sc, 32, 1ll << kSlotTargetLog2));
+  AdaptWs& w = sc->aw;
+  if (npix * 4 > cap) return fail(RTX_ERR_NOMEM, "adaptive render: too many pixels for the device memory");
+  const int32_t kcap = (int32_t)std::min<int64_t>(budget, std::max<int64_t>(4, (cap / npix) & ~3ll));
   int rc;
-  for (int j = 0; j < S; j++) {
-    AdaptWs& w = sc->aw[j];
-    nq[j] = (npix - j + S - 1) / S;
-    if (nq[j] * 4 > cap) return fail(RTX_ERR_NOMEM, "adaptive render: too many pixels for the device memory");
-    kcap[j] = (int32_t)std::min<int64_t>(budget, std::max<int64_t>(4, (cap / nq[j]) & ~3ll));
-    const int64_t slots = nq[j] * (int64_t)kcap[j];
+  {
+    const int64_t slots = npix * (int64_t)kcap;
     if ((rc = w.lbuf.reserve(slots * 3 * sizeof(double)))) return rc;
     if (L.count && (rc = w.segs.reserve(slots * sizeof(uint16_t)))) return rc;
     if ((rc = w.smap.reserve(slots * sizeof(uint2)))) return rc;
     for (DevBuf* b : {&w.k[0], &w.k[1], &w.off})
-      if ((rc = b->reserve(nq[j] * sizeof(uint32_t)))) return rc;
-    if ((rc = w.scan_tmp.reserve(std::max<size_t>(16, rtxscan::temp_bytes(nq[j]))))) return rc;
+      if ((rc = b->reserve(npix * sizeof(uint32_t)))) return rc;
+    if ((rc = w.scan_tmp.reserve(std::max<size_t>(16, rtxscan::temp_bytes(npix))))) return rc;
     if ((rc = w.ctr.reserve(8 * 16 * sizeof(unsigned long long) + 64))) return rc;
     if ((rc = w.total_h.reserve(2 * sizeof(unsigned long long)))) return rc;
     if (!w.ev) HIPC(hipEventCreateWithFlags(&w.ev, hipEventDisableTiming));
-    if (j > 0 && !w.st) HIPC(hipStreamCreateWithFlags(&w.st, hipStreamNonBlocking));
   }
-  auto plan = [&](int j, hipStream_t st, const uint32_t* knext) -> int {  // prefix sum + slot map
-    AdaptWs& w = sc->aw[j];
-    const unsigned qb = (unsigned)((nq[j] + kBlock - 1) / kBlock);
-    HIPC(rtxscan::exclusive_scan_u32(knext, w.off.as<uint32_t>(), nq[j], w.scan_tmp.p, w.scan_tmp.n, st));
-    hipLaunchKernelGGL(k_adapt_expand, dim3(qb), dim3(kBlock), 0, st, knext, (const uint32_t*)w.off.as<uint32_t>(),
-                       nq[j], S, j, (const int32_t*)px.samples, w.smap.as<uint2>(),
-                       w.ctr.as<unsigned long long>() + 8 * 16);
-    HIPC(hipGetLastError());
-    return RTX_OK;
-  };
-  // record + next batch sizes of sub-render j's pixels after phase g (its slots in L: the
-  // uniform first phase's, or the phase's slot map), then the next phase's slot map and count
-  auto record = [&](int j, hipStream_t st, int g, const double* Lph, int64_t active) -> int {
-    AdaptWs& w = sc->aw[j];
+  unsigned long long* ctr = w.ctr.as<unsigned long long>();  // 8 region counters, then the slot count, ...
+  const unsigned qb = (unsigned)((npix + kBlock - 1) / kBlock);
+  // record + next batch sizes after phase g (its slots in Lph: the uniform first phase's, or the
+  // phase's slot map), then the next phase's prefix sum, slot map and (to the host) slot count
+  auto record = [&](int g, const double* Lph, int64_t active) -> int {
     AdaptPlan ap;
     ap.kcur = g == 1 ? nullptr : w.k[g & 1].as<uint32_t>();
     ap.off = g == 1 ? nullptr : w.off.as<uint32_t>();
     ap.knext = w.k[(g + 1) & 1].as<uint32_t>();
-    ap.kuni = K1, ap.sub_n = S, ap.sub_j = j;
-    ap.min_spp = prm->min_spp, ap.budget = budget, ap.phase = g, ap.kcap = kcap[j];
-    // a phase of at least ~kAdaptPhaseSlots slots while pixels remain: once few pixels are left,
+    ap.kuni = K1, ap.sub_n = 1, ap.sub_j = 0;
+    ap.min_spp = prm->min_spp, ap.budget = budget, ap.phase = g, ap.kcap = kcap;
+    // a phase of at least ~phase_slots slots while pixels remain: once few pixels are left,
     // their batches grow (up to the budget) instead of phases that are mostly launch tail
     ap.kmin = (int32_t)std::min<int64_t>(budget, (phase_slots + active - 1) / std::max<int64_t>(1, active));
     ap.rel = prm->rel_threshold;
     ap.margin_step = margin_step;
     ap.segs = !L.count ? nullptr : g == 1 ? sc->segs1.as<uint16_t>() : w.segs.as<uint16_t>();
     ap.rec_segs = A.counters + 9;
-    ap.active = w.ctr.as<unsigned long long>() + 8 * 16 + 1;
-    ap.next_active = w.ctr.as<unsigned long long>() + 8 * 16 + 3;
-    HIPC(hipMemsetAsync(ap.next_active, 0, sizeof(unsigned long long), st));
-    const unsigned qb = (unsigned)((nq[j] + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_adapt_record, dim3(qb), dim3(kBlock), 0, st, px, Lph, nq[j], npix, ap);
+    ap.active = ctr + 8 * 16 + 1;
+    ap.next_active = ctr + 8 * 16 + 3;
+    HIPC(hipMemsetAsync(ap.next_active, 0, sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_adapt_record, dim3(qb), dim3(kBlock), 0, s, px, Lph, npix, npix, ap);
     HIPC(hipGetLastError());
-    hipLaunchKernelGGL(k_adapt_floor, dim3(qb), dim3(kBlock), 0, st, ap.knext, nq[j], S, j,
-                       (const int32_t*)px.samples, budget, kcap[j], (int64_t)phase_slots / S,
-                       (const unsigned long long*)ap.next_active);
+    hipLaunchKernelGGL(k_adapt_floor, dim3(qb), dim3(kBlock), 0, s, ap.knext, npix, 1, 0, (const int32_t*)px.samples,
+                       budget, kcap, phase_slots, (const unsigned long long*)ap.next_active);
     HIPC(hipGetLastError());
-    int rc2;
-    if ((rc2 = plan(j, st, ap.knext))) return rc2;
-    HIPC(hipMemcpyAsync(w.total_h.p, w.ctr.as<unsigned long long>() + 8 * 16, 2 * sizeof(unsigned long long),
-                        hipMemcpyDeviceToHost, st));
-    HIPC(hipEventRecord(w.ev, st));
+    HIPC(rtxscan::exclusive_scan_u32(ap.knext, w.off.as<uint32_t>(), npix, w.scan_tmp.p, w.scan_tmp.n, s));
+    hipLaunchKernelGGL(k_adapt_expand, dim3(qb), dim3(kBlock), 0, s, (const uint32_t*)ap.knext,
+                       (const uint32_t*)w.off.as<uint32_t>(), npix, 1, 0, (const int32_t*)px.samples,
+                       w.smap.as<uint2>(), ctr + 8 * 16);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(w.total_h.p, ctr + 8 * 16, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPC(hipEventRecord(w.ev, s));
     return RTX_OK;
   };
-  // phase 1: min_spp samples of every pixel, one uniform launch over the whole render (the
-  // scene's radiance buffer)
-  {
-    if ((rc = sc->lbuf.reserve((size_t)npix * K1 * 3 * sizeof(double)))) return rc;
-    if (L.count && (rc = sc->segs1.reserve((size_t)npix * K1 * sizeof(uint16_t)))) return rc;
-    RenderArgs A1 = A;
-    A1.L = sc->lbuf.as<double>();
-    A1.conv = nullptr;
-    A1.K = K1, A1.s0 = 0;
-    unsigned long long* ctr = sc->aw[0].ctr.as<unsigned long long>();
+  // one persistent launch of a phase; debug: its time and segments on stderr
+  auto launch = [&](int g, const Launch& Lg, const RenderArgs& Ag, uint16_t* segs, int64_t pixels) -> int {
+    unsigned long long seg0 = 0;
     HIPC(hipMemsetAsync(ctr, 0, 8 * 16 * sizeof(unsigned long long), s));
-    if (debug) HIPC(hipEventRecord(sc->ev[2], s));
-    if ((rc = mark(s))) return rc;
-    if (L.count && (rc = set_segbuf(ctr, sc->segs1.as<uint16_t>(), s))) return rc;
-    if ((rc = persist_m<false>(L, A1, ctr))) return rc;
-    if ((rc = mark(s))) return rc;
+    if (debug) {
+      HIPC(hipStreamSynchronize(s));
+      HIPC(hipMemcpy(&seg0, A.counters, sizeof seg0, hipMemcpyDeviceToHost));
+      HIPC(hipEventRecord(sc->ev[2], s));
+    }
+    int rc2;
+    if ((rc2 = mark(s))) return rc2;
+    if (L.count && (rc2 = set_segbuf(ctr, segs, s))) return rc2;
+    if ((rc2 = persist_m<false>(Lg, Ag, ctr))) return rc2;
+    if ((rc2 = mark(s))) return rc2;
     hot_launches++;
     if (debug) {
       HIPC(hipEventRecord(sc->ev[3], s));
@@ -796,73 +769,35 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
       unsigned long long seg1 = 0;
       HIPC(hipEventElapsedTime(&ms, sc->ev[2], sc->ev[3]));
       HIPC(hipMemcpy(&seg1, A.counters, sizeof seg1, hipMemcpyDeviceToHost));
-      fprintf(stderr, "rtx adaptive: phase 1: %lld pixels x %d samples, launch %.3f ms, %llu segments (%.0f Mseg/s)\n",
-              (long long)npix, K1, ms, seg1, (double)seg1 / (ms * 1e3));
+      fprintf(stderr, "rtx adaptive: phase %d: %lld pixels, launch %.3f ms, %llu segments (%.0f Mseg/s)\n", g,
+              (long long)pixels, ms, seg1 - seg0, (double)(seg1 - seg0) / (ms * 1e3));
     }
-  }
-  if (S > 1) {  // the sub-renders' streams start once the first phase is done
-    for (hipEvent_t* e : {&sc->fork_ev, &sc->join_ev})
-      if (!*e) HIPC(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    HIPC(hipEventRecord(sc->fork_ev, s));
-    for (int j = 1; j < S; j++) HIPC(hipStreamWaitEvent(sc->aw[j].st, sc->fork_ev, 0));
-  }
-  bool alive[kAdaptSubs] = {false, false};
-  for (int j = 0; j < S; j++) {
-    if ((rc = record(j, j == 0 ? s : sc->aw[j].st, 1, sc->lbuf.as<double>(), nq[j]))) return rc;
-    alive[j] = true;
-  }
-  for (int g = 2; alive[0] || alive[1]; g++) {
-    for (int j = 0; j < S; j++) {
-      if (!alive[j]) continue;
-      AdaptWs& w = sc->aw[j];
-      hipStream_t st = j == 0 ? s : w.st;
-      unsigned long long* ctr = w.ctr.as<unsigned long long>();  // 8 region counters, then the slot count
-      // this phase's slot count, computed at the end of the previous one
-      HIPC(hipEventSynchronize(w.ev));
-      const unsigned long long nsl = ((const volatile unsigned long long*)w.total_h.p)[0];
-      const int64_t active = (int64_t)((const volatile unsigned long long*)w.total_h.p)[1];
-      if (debug) fprintf(stderr, "rtx adaptive: sub-render %d phase %d: %lld pixels, %llu slots\n", j, g, (long long)active, nsl);
-      if (nsl == 0) {
-        alive[j] = false;
-        continue;
-      }
-      RenderArgs Aj = A;
-      Aj.L = w.lbuf.as<double>();
-      Aj.conv = nullptr;  // only pixels still sampling have slots
-      Aj.K = 1, Aj.s0 = 0;  // (unused: slots from the phase's slot map)
-      Launch Lj = L;
-      Lj.s = st;
-      Lj.map = true;
-      HIPC(hipMemsetAsync(ctr, 0, 8 * 16 * sizeof(unsigned long long), st));
-      unsigned long long seg0 = 0;
-      if (debug) {
-        HIPC(hipStreamSynchronize(st));
-        HIPC(hipMemcpy(&seg0, A.counters, sizeof seg0, hipMemcpyDeviceToHost));
-        HIPC(hipEventRecord(sc->ev[2], st));
-      }
-      if ((rc = mark(st))) return rc;
-      if (L.count && (rc = set_segbuf(ctr, w.segs.as<uint16_t>(), st))) return rc;
-      if ((rc = persist_m<false>(Lj, Aj, ctr))) return rc;
-      if ((rc = mark(st))) return rc;
-      hot_launches++;
-      if (debug) {
-        HIPC(hipEventRecord(sc->ev[3], st));
-        HIPC(hipEventSynchronize(sc->ev[3]));
-        float ms = 0;
-        unsigned long long seg1 = 0;
-        HIPC(hipEventElapsedTime(&ms, sc->ev[2], sc->ev[3]));
-        HIPC(hipMemcpy(&seg1, A.counters, sizeof seg1, hipMemcpyDeviceToHost));
-        fprintf(stderr, "rtx adaptive:   phase %d launch %.3f ms, %llu segments (%.0f Mseg/s; other sub-renders' included)\n",
-                g, ms, seg1 - seg0, (double)(seg1 - seg0) / (ms * 1e3));
-      }
-      if ((rc = record(j, st, g, Aj.L, active))) return rc;
-    }
-  }
-  if (S > 1) {  // s continues once every sub-render is done
-    for (int j = 1; j < S; j++) {
-      HIPC(hipEventRecord(sc->join_ev, sc->aw[j].st));
-      HIPC(hipStreamWaitEvent(s, sc->join_ev, 0));
-    }
+    return RTX_OK;
+  };
+  // phase 1: min_spp samples of every pixel, one uniform launch over the whole render (the
+  // scene's radiance buffer)
+  if ((rc = sc->lbuf.reserve((size_t)npix * K1 * 3 * sizeof(double)))) return rc;
+  if (L.count && (rc = sc->segs1.reserve((size_t)npix * K1 * sizeof(uint16_t)))) return rc;
+  RenderArgs A1 = A;
+  A1.L = sc->lbuf.as<double>();
+  A1.conv = nullptr;
+  A1.K = K1, A1.s0 = 0;
+  if ((rc = launch(1, L, A1, sc->segs1.as<uint16_t>(), npix))) return rc;
+  if ((rc = record(1, sc->lbuf.as<double>(), npix))) return rc;
+  RenderArgs Ag = A;
+  Ag.L = w.lbuf.as<double>();
+  Ag.conv = nullptr;    // only pixels still sampling have slots
+  Ag.K = 1, Ag.s0 = 0;  // (unused: slots from the phase's slot map)
+  Launch Lg = L;
+  Lg.map = true;
+  for (int g = 2;; g++) {
+    // this phase's slot count, computed at the end of the previous one
+    HIPC(hipEventSynchronize(w.ev));
+    const unsigned long long nsl = ((const volatile unsigned long long*)w.total_h.p)[0];
+    const int64_t active = (int64_t)((const volatile unsigned long long*)w.total_h.p)[1];
+    if (nsl == 0) break;
+    if ((rc = launch(g, Lg, Ag, w.segs.as<uint16_t>(), active))) return rc;
+    if ((rc = record(g, Ag.L, active))) return rc;
   }
   return RTX_OK;
 }

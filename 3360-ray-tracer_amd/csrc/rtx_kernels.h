@@ -638,7 +638,7 @@ __device__ __forceinline__ uint32_t adapt_next_batch(const double (&mean)[3], co
 // the running count), so the parallelism is across pixels, and each lane streams its own run
 // of the phase's slots with the loads of the next kRecAhead samples in flight while it
 // replays the current one (a lane's run is contiguous: its loads walk the same cache lines).
-constexpr int kRecAhead = 4;
+constexpr int kRecAhead = 8;
 __global__ __launch_bounds__(kBlock) void k_adapt_record(PixelSoA px, const double* __restrict__ L, int64_t nq,
                                                          int64_t npix, AdaptPlan ap) {
   const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -666,12 +666,21 @@ __global__ __launch_bounds__(kBlock) void k_adapt_record(PixelSoA px, const doub
       }
       for (int c = 0; c < 3; c++) sum[c] += x[c];
       if (n >= ap.min_spp) {
+        // err / mu > rel  <=>  m2 > rel^2 (n - 1) n mu^2 up to the few ulps the exact form rounds
+        // by: decided by products where the two sides differ by more than 1e-10 relative (the
+        // usual case), the exact form (two divisions, two square roots) only in between; NaN
+        // fails both comparisons and takes the exact form too.
         bool ok = true;
         for (int c = 0; c < 3 && ok; c++) {
-          double var = n > 1 ? m2[c] / (n - 1) : 0.0;
           double mu = fmax(fabs(mean[c]), 1e-3);
-          double err = sqrt(var) / sqrt((double)n);
-          if (err / mu > ap.rel) ok = false;
+          const double thr = ap.rel * ap.rel * ((double)(n - 1) * (double)n * (mu * mu));
+          if (m2[c] > thr * (1.0 + 1e-10)) {
+            ok = false;
+          } else if (!(m2[c] < thr * (1.0 - 1e-10))) {
+            double var = n > 1 ? m2[c] / (n - 1) : 0.0;
+            double err = sqrt(var) / sqrt((double)n);
+            if (err / mu > ap.rel) ok = false;
+          }
         }
         conv = ok;
       }
