@@ -108,7 +108,7 @@ constexpr int kBands = 8;  // bands of the last accumulate and of the D2H copies
 
 // Adaptive renders in phases (render_adaptive)
 constexpr int64_t kAdaptPhaseSlots = 1 << 23;  // render_adaptive: smallest phase planned while pixels remain (ab r3x/r3y: 2^21..2^25)
-constexpr double kAdaptMarginStep = 0.25;      // render_adaptive: batch margin 1 + step * (phase - 1)
+constexpr double kAdaptMarginStep = 0.25;      // render_adaptive: batch margin 1 + step * (phase - 1) (0.5: within noise, r3y)
 struct AdaptWs {
   DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer
   DevBuf segs;                                  // counting renders: each slot's path segments (u16)
@@ -688,11 +688,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   const int64_t npix = A.npix;
   const int K1 = std::min(std::max(1, prm->min_spp), budget);
   static const bool debug = std::getenv("RTX_DEBUG_ADAPT") != nullptr;  // per-phase slot counts on stderr
-  // tuning (A/B only): the smallest phase (log2 slots) and the per-phase batch margin step
-  static const char* ps_env = std::getenv("RTX_ADAPT_PHASE_SLOTS_LOG2");
-  static const char* mg_env = std::getenv("RTX_ADAPT_MARGIN_STEP");
-  const int64_t phase_slots = ps_env ? (1ll << std::min(30, std::max(10, std::atoi(ps_env)))) : kAdaptPhaseSlots;
-  const double margin_step = mg_env ? std::max(0.0, std::atof(mg_env)) : kAdaptMarginStep;
+  const int64_t phase_slots = kAdaptPhaseSlots;
   if ((int64_t)npix * K1 > 0xFFFFFFFFll) return fail(RTX_ERR_INVALID, "adaptive render: npix x min_spp above 2^32");
   // slots after the first phase: 24 B of radiance + 8 B of slot map each
   const int64_t cap = std::min<int64_t>(0xFFFFFFFFll, slot_target(sc, 32, 1ll << kSlotTargetLog2));
@@ -727,7 +723,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     // their batches grow (up to the budget) instead of phases that are mostly launch tail
     ap.kmin = (int32_t)std::min<int64_t>(budget, (phase_slots + active - 1) / std::max<int64_t>(1, active));
     ap.rel = prm->rel_threshold;
-    ap.margin_step = margin_step;
+    ap.margin_step = kAdaptMarginStep;
     ap.segs = !L.count ? nullptr : g == 1 ? sc->segs1.as<uint16_t>() : w.segs.as<uint16_t>();
     ap.rec_segs = A.counters + 9;
     ap.active = ctr + 8 * 16 + 1;

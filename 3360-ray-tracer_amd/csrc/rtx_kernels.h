@@ -399,19 +399,26 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
     }
     // ---- start the primary path of a freshly assigned slot ----
     if (fresh) {
+      // The primary's inputs (camera, pixel map, group) are read from the kernel argument
+      // segment here (A is the kernel's first argument, at offset 0), through a pointer the
+      // compiler cannot see through, so they are not held in registers across the walk: the
+      // kernel runs at the SGPR limit (C3 build: 79 -> 64 spilled SGPRs, no scratch).
+      auto kseg = __builtin_amdgcn_kernarg_segment_ptr();
+      asm volatile("" : "+s"(kseg));
+      const RenderArgs& Ar = *(const RenderArgs*)kseg;
       // nslots < 2^32 (checked on the host): 32-bit division
       uint2 e = make_uint2(0u, 0u);
       if (MAP) e = ((const uint2*)next_slot[8 * 16 + 2])[slot];
-      const uint32_t p = MAP ? e.x : (uint32_t)slot / (uint32_t)A.K;
-      if (!(A.conv && A.conv[p])) {
-        const int k = MAP ? 0 : (int)((uint32_t)slot - p * (uint32_t)A.K);
+      const uint32_t p = MAP ? e.x : (uint32_t)slot / (uint32_t)Ar.K;
+      if (!(Ar.conv && Ar.conv[p])) {
+        const int k = MAP ? 0 : (int)((uint32_t)slot - p * (uint32_t)Ar.K);
         int x, y;
-        A.map.xy(p, x, y);
-        pix = (uint32_t)(y * A.map.W + x), smp = MAP ? e.y : (uint32_t)(A.s0 + k);
+        Ar.map.xy(p, x, y);
+        pix = (uint32_t)(y * Ar.map.W + x), smp = MAP ? e.y : (uint32_t)(Ar.s0 + k);
         Rng g = make_rng(A.seed, pix, smp, 0u);
-        get_ray<NODOF>(A.cam, x, y, g, P.o, P.d);
+        get_ray<NODOF>(Ar.cam, x, y, g, P.o, P.d);
         thr_lds[0] = 1.0, thr_lds[kBlock] = 1.0, thr_lds[2 * kBlock] = 1.0;
-        P.depth = SCATTER ? A.max_depth : 0;
+        P.depth = SCATTER ? Ar.max_depth : 0;
         has = true;
         prims++;
         if (COUNT) pseg = 0;
