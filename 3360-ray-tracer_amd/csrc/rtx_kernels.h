@@ -402,10 +402,14 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
       // The primary's inputs (camera, pixel map, group) are read from the kernel argument
       // segment here (A is the kernel's first argument, at offset 0), through a pointer the
       // compiler cannot see through, so they are not held in registers across the walk: the
-      // kernel runs at the SGPR limit (C3 build: 79 -> 64 spilled SGPRs, no scratch).
+      // kernel runs at the SGPR limit (generic PARK build: +4.3 %, C2 +0.7 %, C5 +-0, its
+      // scratch 80 -> 16 B; the bunny's Lambertian texture-free builds lost 1.0 % (their spilled
+      // SGPRs 79 -> 60, scratch 52 -> 0 B), so they keep the arguments in registers;
+      // profiles/r03/ab_kernarg_refill_r4g_*).
+      constexpr bool kArgsAtRefill = !(LAMB && NOTEX);
       auto kseg = __builtin_amdgcn_kernarg_segment_ptr();
-      asm volatile("" : "+s"(kseg));
-      const RenderArgs& Ar = *(const RenderArgs*)kseg;
+      if (kArgsAtRefill) asm volatile("" : "+s"(kseg));
+      const RenderArgs& Ar = kArgsAtRefill ? *(const RenderArgs*)kseg : A;
       // nslots < 2^32 (checked on the host): 32-bit division
       uint2 e = make_uint2(0u, 0u);
       if (MAP) e = ((const uint2*)next_slot[8 * 16 + 2])[slot];
