@@ -141,6 +141,7 @@ struct rtx_scene {
   DevBuf px_sum, px_mean, px_m2, px_samples, px_conv, lbuf, queue[2], counters, out_rgb, out_spp, rays, hits;
   DevBuf p3_scratch, p3_body;  // device P3 encoding (rtx_p3.h)
   HostBuf stage_rgb, stage_spp;  // rtx_render_multi: pinned D2H staging of this device's stripes
+  HostBuf counters_h;            // timed renders: pinned copy of the statistics counters (read after the end event)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> evpool;
   // banded output copies (BandSink): a copy stream and its ordering events
@@ -1341,7 +1342,11 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
                        prm->mode == RTX_MODE_MEGAKERNEL ? (mk_adaptive ? 2 : 1) : 0, prm->spp, d_rgb, d_spp);
     HIPC(hipGetLastError());
   }
-  if (timed) HIPC(hipEventRecord(sc->ev[1], s));
+  if (timed) {  // the statistics come back with the frame: one wait on the end event, no blocking copy after it
+    if ((rc = sc->counters_h.reserve(10 * sizeof(unsigned long long)))) return rc;
+    HIPC(hipMemcpyAsync(sc->counters_h.p, cnt, 10 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPC(hipEventRecord(sc->ev[1], s));
+  }
   if (banded) {  // the caller's stream owns the output again once the band copies are done
     HIPC(hipEventRecord(sc->band_ev[kBands], sc->copy_stream));
     HIPC(hipStreamWaitEvent(s, sc->band_ev[kBands], 0));
@@ -1358,7 +1363,7 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
       hot_ms += hms;
     }
     unsigned long long h[10];
-    HIPC(hipMemcpy(h, cnt, sizeof h, hipMemcpyDeviceToHost));
+    std::memcpy(h, sc->counters_h.p, sizeof h);
     stats->rays_total = h[0];
     stats->parked = L.park ? 1 : 0;
     stats->rays_primary = h[1];

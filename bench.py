@@ -278,7 +278,8 @@ def main():
         gst = [step(gp) for _ in range(g_steps)]
         torch.cuda.synchronize()
         tg = time.perf_counter() - tg
-        generic_leg = {"value": sum(s["rays_total"] for s in gst) / tg / 1e6, "ms_per_step": tg * 1e3 / g_steps,
+        g_rays = cst["rays_recorded"] * g_steps if args.adaptive else sum(s["rays_total"] for s in gst)
+        generic_leg = {"value": g_rays / tg / 1e6, "ms_per_step": tg * 1e3 / g_steps,
                        "steps": g_steps, "build": rtx.build_names(gst[-1]["build"]),
                        "note": "same frame with RTX_FLAG_GENERIC: no per-scene specialisation (same pixels)"}
 
