@@ -109,13 +109,33 @@ constexpr int kBands = 8;  // bands of the last accumulate and of the D2H copies
 // Adaptive renders in phases (render_adaptive)
 constexpr int64_t kAdaptPhaseSlots = 1 << 23;  // render_adaptive: smallest phase planned while pixels remain (ab r3x/r3y: 2^21..2^25)
 constexpr double kAdaptMarginStep = 0.25;      // render_adaptive: batch margin 1 + step * (phase - 1) (0.5: within noise, r3y)
+// The tile schedule (rtx_kernels.h, TileArgs): the largest batch of one pixel, the smallest
+// further batch of a pixel not yet converged, and the batch margin over the predicted need.
+constexpr int kTileKcap = 128;
+constexpr int kTileKinc = 8;
+constexpr double kTileMargin = 1.0;
+// Overrides of the adaptive schedules' constants (0: the default): rtx_internal_adapt_tune, a
+// test and tuning hook (not in rtx.h) that forces small workspaces and floors, so the paths
+// that only a large frame at a large budget reaches run on small frames too.
+struct AdaptTune {
+  int tile_kcap, tile_kinc;
+  double tile_margin;
+  int64_t phase_slots;  // phases: the smallest phase planned while pixels remain (kAdaptPhaseSlots)
+  int phase_kcap;       // phases: the largest batch of one pixel (else from the workspace)
+};
+static AdaptTune g_tune{};
 struct AdaptWs {
-  DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer
+  DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer, [134] TileArgs
   DevBuf segs;                                  // counting renders: each slot's path segments (u16)
+  // the tile schedule: active pixels, the claim-order sort's keys / values (in, out) and its
+  // temporary storage, per-region tile counts [0..8) + active pixel count [8], TileArgs
+  DevBuf act, tkeys[2], tvals[2], sort_tmp, tcount, targs;
   HostBuf total_h;                              // pinned copy of the next phase's slot count
   hipEvent_t ev = nullptr;                      // total_h written
   void release() {
-    for (DevBuf* b : {&lbuf, &smap, &k[0], &k[1], &off, &scan_tmp, &ctr, &segs}) b->release();
+    for (DevBuf* b : {&lbuf, &smap, &k[0], &k[1], &off, &scan_tmp, &ctr, &segs, &act, &tkeys[0], &tkeys[1], &tvals[0],
+                      &tvals[1], &sort_tmp, &tcount, &targs})
+      b->release();
     total_h.release();
     if (ev) (void)hipEventDestroy(ev);
     ev = nullptr;
@@ -563,7 +583,8 @@ struct Launch {
   bool fast, count;
   int park = 0;  // persistent: 0 plain kernel, PARK kernel (parked traversals) with 1 the leaf-step, 2 the speculative walk
   bool generic = false;  // RTX_FLAG_GENERIC: no per-scene specialisation (TK, LAMB, NOTEX, NODOF)
-  bool map = false;      // adaptive phases: slots from the phase's slot map (k_persistent MAP)
+  int map = 0;           // k_persistent MAP: 0 uniform groups, 1 an adaptive phase's slot map, 2 adaptive tiles
+  int max_grid = 0;      // > 0: at most this many blocks (the tile schedule's workspace has room for them)
   mutable uint32_t build = 0;  // RTX_BUILD_* bits of the persistent instantiation launched last
 };
 
@@ -579,12 +600,13 @@ int run_extend(const Launch& L, const RenderArgs& A, const PathQueue& q, const u
 }
 
 template <int STACK, bool FAST, bool COUNT, bool SCATTER, int PARK, int TK, bool LAMB, bool NOTEX, bool NODOF,
-          bool MAP>
+          int MAP>
 int run_persistent_k1(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
   if (A.stack_slots < 1 || A.stack_slots > STACK + 1) return fail(RTX_ERR_INVALID, "bad traversal stack size");
-  const size_t lds = persist_lds(A.stack_slots, spec_walk(PARK, FAST, SCATTER)).end;
-  const int grid = persistent_grid(
+  const size_t lds = persist_lds(A.stack_slots, spec_walk(PARK, FAST, SCATTER), MAP == 2).end;
+  int grid = persistent_grid(
       L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF, MAP>, lds);
+  if (L.max_grid > 0) grid = std::min(grid, L.max_grid);
   L.build = (PARK ? RTX_BUILD_PARK : 0u) | (PARK == 2 ? RTX_BUILD_SPECULATIVE : 0u) | (TK == (int)RTX_PRIM_SPHERE ? RTX_BUILD_SPHERE_TREE : 0u) |
             (TK == (int)RTX_PRIM_TRIANGLE ? RTX_BUILD_TRIANGLE_TREE : 0u) | (LAMB ? RTX_BUILD_LAMBERTIAN : 0u) |
             (NOTEX ? RTX_BUILD_NO_TEXTURES : 0u) | (NODOF ? RTX_BUILD_NO_DEFOCUS : 0u) |
@@ -597,14 +619,17 @@ int run_persistent_k1(const Launch& L, const RenderArgs& A, unsigned long long* 
   HIPC(hipGetLastError());
   return RTX_OK;
 }
-// adaptive phases draw their slots from a slot map (L.map; never with the scatter API)
+// adaptive renders draw their slots from a slot map or the tile schedule (L.map; never with the
+// scatter API)
 template <int STACK, bool FAST, bool COUNT, bool SCATTER, int PARK, int TK, bool LAMB = false, bool NOTEX = false,
           bool NODOF = false>
 int run_persistent_k0(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
-  if (!SCATTER && L.map)
-    return run_persistent_k1<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF, !SCATTER>(L, A, next_slot);
+  if (!SCATTER && L.map == 1)
+    return run_persistent_k1<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF, SCATTER ? 0 : 1>(L, A, next_slot);
+  if (!SCATTER && L.map == 2)
+    return run_persistent_k1<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF, SCATTER ? 0 : 2>(L, A, next_slot);
   if (L.map) return fail(RTX_ERR_INVALID, "slot maps are not used with the scatter API");
-  return run_persistent_k1<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF, false>(L, A, next_slot);
+  return run_persistent_k1<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF, 0>(L, A, next_slot);
 }
 // the texture-free plain build also comes without the camera's thin-lens sampling (defocus
 // off; C2 +1.0 %; the PARK build lost 2.8 % with it, ab_nodof_*)
@@ -673,31 +698,56 @@ int set_segbuf(unsigned long long* ctr, uint16_t* segs, hipStream_t st) {
   HIPC(hipMemsetD32Async((hipDeviceptr_t)(w + 1), (int)(uint32_t)(v >> 32), 1, st));
   return RTX_OK;
 }
-// Adaptive sampling in phases on the persistent kernel (rtx_kernels.h, "Adaptive sampling in
-// phases"): the reference's WavefrontRenderer::Render loop (wavefront.cc:57-225, always
-// adaptive) with the same per-pixel results, on the caller's stream `s`: phase 1, min_spp
-// samples of every pixel; then, after each phase, record + next batch sizes (k_adapt_record,
-// k_adapt_floor); before each phase, prefix sum and slot map (k_adapt_expand); the host reads
-// the next phase's slot count (one pinned word) to launch it or stop.  `mark` records a
-// hot-kernel timing event (before and after each persistent launch); hot_launches counts them.
-// The caller resolves the pixels (k_resolve).  (Round 3 also ran the pixels as two interleaved
-// sub-renders on two streams, meant to fill one's phase ends with the other's tracing: one
-// sequence is faster, C3 14.9 vs 15.7 ms per frame, DESIGN.md.)
+// Adaptive sampling on the persistent kernel: the reference's WavefrontRenderer::Render loop
+// (wavefront.cc:57-225, always adaptive) with the same per-pixel results, on the caller's
+// stream `s`.  Phase 1 traces min_spp samples of every pixel (one uniform launch) and
+// k_adapt_record replays them and sizes each pixel's next batch.  Then either
+//  * tiles (the default; rtx_kernels.h "tile schedule"): the pixels still sampling are cut into
+//    tiles, ordered per region largest predicted work first (flag, scan, compact, keys, radix
+//    sort: all on the stream, no host round trip), and ONE more persistent launch runs every
+//    further phase of every tile, each tile's record inside the workgroup that traces it; or
+//  * phases (RTX_FLAG_ADAPT_PHASES; round 3's schedule): after each phase, record + next batch
+//    sizes (k_adapt_record, k_adapt_floor); before each phase, prefix sum and slot map
+//    (k_adapt_expand); the host reads the next phase's slot count (one pinned word) to launch it
+//    or stop; every phase is a launch of its own with its own drain.
+// `mark` records a hot-kernel timing event (before and after each persistent launch);
+// hot_launches counts them.  The caller resolves the pixels (k_resolve).
 template <class Mark>
 int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const rtx_render_params* prm,
                     const PixelSoA& px, int budget, hipStream_t s, Mark mark, uint64_t& hot_launches) {
   const int64_t npix = A.npix;
   const int K1 = std::min(std::max(1, prm->min_spp), budget);
   static const bool debug = std::getenv("RTX_DEBUG_ADAPT") != nullptr;  // per-phase slot counts on stderr
-  const int64_t phase_slots = kAdaptPhaseSlots;
+  const bool tiles = !(prm->flags & RTX_FLAG_ADAPT_PHASES);
+  const int64_t phase_slots = g_tune.phase_slots > 0 ? g_tune.phase_slots : kAdaptPhaseSlots;
   if ((int64_t)npix * K1 > 0xFFFFFFFFll) return fail(RTX_ERR_INVALID, "adaptive render: npix x min_spp above 2^32");
-  // slots after the first phase: 24 B of radiance + 8 B of slot map each
-  const int64_t cap = std::min<int64_t>(0xFFFFFFFFll, slot_target(sc, 32, 1ll << kSlotTargetLog2));
   AdaptWs& w = sc->aw;
-  if (npix * 4 > cap) return fail(RTX_ERR_NOMEM, "adaptive render: too many pixels for the device memory");
-  const int32_t kcap = (int32_t)std::min<int64_t>(budget, std::max<int64_t>(4, (cap / npix) & ~3ll));
   int rc;
-  {
+  // tile schedule: room for every block the launch can hold (4 per CU at 128 VGPRs), each with
+  // kTileNT tiles of kTileTP pixels x kcap slots (24 B of radiance each)
+  const int64_t max_blocks = 4ll * sc->cus;
+  const int64_t max_tiles = (npix + kTileTP - 1) / kTileTP;
+  int32_t kcap;
+  if (tiles) {
+    kcap = std::max(1, std::min(budget, g_tune.tile_kcap > 0 ? g_tune.tile_kcap : kTileKcap));
+    const int64_t slots = max_blocks * kTileNT * kTileTP * (int64_t)kcap;
+    if ((rc = w.lbuf.reserve(slots * 3 * sizeof(double)))) return rc;
+    if (L.count && (rc = w.segs.reserve(slots * sizeof(uint16_t)))) return rc;
+    for (DevBuf* b : {&w.k[0], &w.k[1], &w.off, &w.act})
+      if ((rc = b->reserve(npix * sizeof(uint32_t)))) return rc;
+    for (DevBuf* b : {&w.tkeys[0], &w.tkeys[1], &w.tvals[0], &w.tvals[1]})
+      if ((rc = b->reserve(std::max<int64_t>(1, max_tiles) * sizeof(uint32_t)))) return rc;
+    if ((rc = w.scan_tmp.reserve(std::max<size_t>(16, rtxscan::temp_bytes(npix))))) return rc;
+    if ((rc = w.sort_tmp.reserve(std::max<size_t>(16, rtxscan::sort_temp_bytes(max_tiles))))) return rc;
+    if ((rc = w.tcount.reserve(16 * sizeof(uint32_t)))) return rc;
+    if ((rc = w.targs.reserve(sizeof(TileArgs)))) return rc;
+    if ((rc = w.ctr.reserve(8 * 16 * sizeof(unsigned long long) + 64))) return rc;
+  } else {
+    // slots after the first phase: 24 B of radiance + 8 B of slot map each
+    const int64_t cap = std::min<int64_t>(0xFFFFFFFFll, slot_target(sc, 32, 1ll << kSlotTargetLog2));
+    if (npix * 4 > cap) return fail(RTX_ERR_NOMEM, "adaptive render: too many pixels for the device memory");
+    kcap = (int32_t)std::min<int64_t>(budget, std::max<int64_t>(4, (cap / npix) & ~3ll));
+    if (g_tune.phase_kcap > 0) kcap = std::min(kcap, g_tune.phase_kcap);
     const int64_t slots = npix * (int64_t)kcap;
     if ((rc = w.lbuf.reserve(slots * 3 * sizeof(double)))) return rc;
     if (L.count && (rc = w.segs.reserve(slots * sizeof(uint16_t)))) return rc;
@@ -709,10 +759,13 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     if ((rc = w.total_h.reserve(2 * sizeof(unsigned long long)))) return rc;
     if (!w.ev) HIPC(hipEventCreateWithFlags(&w.ev, hipEventDisableTiming));
   }
+  const double tile_margin = g_tune.tile_margin > 0 ? g_tune.tile_margin : kTileMargin;
+  const int32_t tile_kinc = g_tune.tile_kinc > 0 ? g_tune.tile_kinc : kTileKinc;
   unsigned long long* ctr = w.ctr.as<unsigned long long>();  // 8 region counters, then the slot count, ...
   const unsigned qb = (unsigned)((npix + kBlock - 1) / kBlock);
   // record + next batch sizes after phase g (its slots in Lph: the uniform first phase's, or the
-  // phase's slot map), then the next phase's prefix sum, slot map and (to the host) slot count
+  // phase's slot map), then (phases) the next phase's prefix sum, slot map and (to the host)
+  // slot count
   auto record = [&](int g, const double* Lph, int64_t active) -> int {
     AdaptPlan ap;
     ap.kcur = g == 1 ? nullptr : w.k[g & 1].as<uint32_t>();
@@ -720,9 +773,11 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ap.knext = w.k[(g + 1) & 1].as<uint32_t>();
     ap.kuni = K1, ap.sub_n = 1, ap.sub_j = 0;
     ap.min_spp = prm->min_spp, ap.budget = budget, ap.phase = g, ap.kcap = kcap;
-    // a phase of at least ~phase_slots slots while pixels remain: once few pixels are left,
-    // their batches grow (up to the budget) instead of phases that are mostly launch tail
-    ap.kmin = (int32_t)std::min<int64_t>(budget, (phase_slots + active - 1) / std::max<int64_t>(1, active));
+    // phases: a phase of at least ~phase_slots slots while pixels remain: once few pixels are
+    // left, their batches grow (up to the budget) instead of phases that are mostly launch
+    // tail; tiles: the smallest batch only (phase ends cost no drain)
+    ap.kmin = tiles ? tile_kinc
+                    : (int32_t)std::min<int64_t>(budget, (phase_slots + active - 1) / std::max<int64_t>(1, active));
     ap.rel = prm->rel_threshold;
     ap.margin_step = kAdaptMarginStep;
     ap.segs = !L.count ? nullptr : g == 1 ? sc->segs1.as<uint16_t>() : w.segs.as<uint16_t>();
@@ -732,6 +787,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     HIPC(hipMemsetAsync(ap.next_active, 0, sizeof(unsigned long long), s));
     hipLaunchKernelGGL(k_adapt_record, dim3(qb), dim3(kBlock), 0, s, px, Lph, npix, npix, ap);
     HIPC(hipGetLastError());
+    if (tiles) return RTX_OK;
     hipLaunchKernelGGL(k_adapt_floor, dim3(qb), dim3(kBlock), 0, s, ap.knext, npix, 1, 0, (const int32_t*)px.samples,
                        budget, kcap, phase_slots, (const unsigned long long*)ap.next_active);
     HIPC(hipGetLastError());
@@ -755,7 +811,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     }
     int rc2;
     if ((rc2 = mark(s))) return rc2;
-    if (L.count && (rc2 = set_segbuf(ctr, segs, s))) return rc2;
+    if (L.count && Lg.map != 2 && (rc2 = set_segbuf(ctr, segs, s))) return rc2;
     if ((rc2 = persist_m<false>(Lg, Ag, ctr))) return rc2;
     if ((rc2 = mark(s))) return rc2;
     hot_launches++;
@@ -766,8 +822,14 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
       unsigned long long seg1 = 0;
       HIPC(hipEventElapsedTime(&ms, sc->ev[2], sc->ev[3]));
       HIPC(hipMemcpy(&seg1, A.counters, sizeof seg1, hipMemcpyDeviceToHost));
-      fprintf(stderr, "rtx adaptive: phase %d: %lld pixels, launch %.3f ms, %llu segments (%.0f Mseg/s)\n", g,
-              (long long)pixels, ms, seg1 - seg0, (double)(seg1 - seg0) / (ms * 1e3));
+      if (Lg.map == 2) {
+        uint32_t tc[9] = {};
+        HIPC(hipMemcpy(tc, w.tcount.p, sizeof tc, hipMemcpyDeviceToHost));
+        pixels = tc[8];
+      }
+      fprintf(stderr, "rtx adaptive: %s %d: %lld pixels, launch %.3f ms, %llu segments (%.0f Mseg/s)\n",
+              Lg.map == 2 ? "tiles after phase" : "phase", g, (long long)pixels, ms, seg1 - seg0,
+              (double)(seg1 - seg0) / (ms * 1e3));
     }
     return RTX_OK;
   };
@@ -784,9 +846,45 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   RenderArgs Ag = A;
   Ag.L = w.lbuf.as<double>();
   Ag.conv = nullptr;    // only pixels still sampling have slots
-  Ag.K = 1, Ag.s0 = 0;  // (unused: slots from the phase's slot map)
+  Ag.K = 1, Ag.s0 = 0;  // (unused: slots from the phase's slot map / the tiles)
   Launch Lg = L;
-  Lg.map = true;
+  if (tiles) {
+    // the claim order: active pixels (knext != 0) compacted in image order, tiles keyed by
+    // (region, work descending), sorted; then the one launch of every further phase
+    uint32_t* knext = w.k[0].as<uint32_t>();  // record(1) wrote the first batches here
+    uint32_t* flag = w.k[1].as<uint32_t>();
+    uint32_t* tc = w.tcount.as<uint32_t>();
+    hipLaunchKernelGGL(k_tile_flags, dim3(qb), dim3(kBlock), 0, s, (const uint32_t*)knext, npix, flag);
+    HIPC(hipGetLastError());
+    HIPC(rtxscan::exclusive_scan_u32(flag, w.off.as<uint32_t>(), npix, w.scan_tmp.p, w.scan_tmp.n, s));
+    HIPC(hipMemsetAsync(tc, 0, 16 * sizeof(uint32_t), s));
+    hipLaunchKernelGGL(k_tile_compact, dim3(qb), dim3(kBlock), 0, s, (const uint32_t*)flag,
+                       (const uint32_t*)w.off.as<uint32_t>(), npix, w.act.as<uint32_t>(), tc + 8);
+    HIPC(hipGetLastError());
+    const unsigned tb = (unsigned)std::max<int64_t>(1, (max_tiles + kBlock - 1) / kBlock);
+    hipLaunchKernelGGL(k_tile_keys, dim3(tb), dim3(kBlock), 0, s, (const uint32_t*)w.act.as<uint32_t>(),
+                       (const uint32_t*)(tc + 8), (const uint32_t*)knext, npix, max_tiles, w.tkeys[0].as<uint32_t>(),
+                       w.tvals[0].as<uint32_t>(), tc);
+    HIPC(hipGetLastError());
+    HIPC(rtxscan::sort_pairs_u32(w.tkeys[0].as<uint32_t>(), w.tkeys[1].as<uint32_t>(), w.tvals[0].as<uint32_t>(),
+                                 w.tvals[1].as<uint32_t>(), max_tiles, w.sort_tmp.p, w.sort_tmp.n, s));
+    TileArgs ta{};
+    ta.act = w.act.as<uint32_t>(), ta.order = w.tvals[1].as<uint32_t>(), ta.rcount = tc, ta.knext = knext;
+    ta.nact = tc + 8;
+    ta.L = w.lbuf.as<double>();
+    ta.segs = L.count ? w.segs.as<uint16_t>() : nullptr;
+    ta.rec_segs = A.counters + 9;
+    ta.px = px, ta.npix = npix;
+    ta.kcap = kcap, ta.min_spp = prm->min_spp, ta.budget = budget, ta.kinc = tile_kinc;
+    ta.max_blocks = (int32_t)max_blocks;
+    ta.rel = prm->rel_threshold, ta.margin = tile_margin;
+    hipLaunchKernelGGL(k_tile_setup, dim3(1), dim3(1), 0, s, ta, w.targs.as<TileArgs>(), ctr);
+    HIPC(hipGetLastError());
+    Lg.map = 2;
+    Lg.max_grid = (int)max_blocks;
+    return launch(2, Lg, Ag, nullptr, 0);
+  }
+  Lg.map = 1;
   for (int g = 2;; g++) {
     // this phase's slot count, computed at the end of the previous one
     HIPC(hipEventSynchronize(w.ev));
@@ -1699,19 +1797,35 @@ extern "C" int rtx_internal_check_sincos(int device, int64_t n, uint64_t seed, i
   return RTX_OK;
 }
 
+// Test / tuning hook (not in rtx.h): overrides of the adaptive schedules' constants for the
+// renders that follow in this process (0 restores a default): the tile schedule's largest and
+// smallest batch of a pixel and its batch margin; the phase schedule's smallest phase and
+// largest batch.  Results never depend on them, only the amount of work and the number of
+// phases do (tests/test_gpu_timed.py runs the full budgets through forced small workspaces).
+extern "C" int rtx_internal_adapt_tune(int32_t tile_kcap, int32_t tile_kinc, double tile_margin, int64_t phase_slots,
+                                       int32_t phase_kcap) {
+  if (tile_kcap < 0 || tile_kinc < 0 || !(tile_margin >= 0) || phase_slots < 0 || phase_kcap < 0)
+    return fail(RTX_ERR_INVALID, "negative tuning value");
+  g_tune = AdaptTune{tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap};
+  return RTX_OK;
+}
+
 // Test hook (not in rtx.h): the persistent kernel's LDS layout (persist_lds) for a traversal
 // stack of stack_slots entries per lane and a schedule (park: 0 plain, 1 PARK with the
-// leaf-step walk, 2 PARK with the speculative walk): out[0..4] = byte offsets of the stack, throughput, hit point,
-// leaf queue and the block's LDS size; out[5..8] = each region's bytes per lane (entries x
-// element size), the regions being lane-interleaved with stride kBlock.  tests/
-// test_capi_exports.py checks that the regions are disjoint and inside the block's LDS for every
-// stack size the host can choose.
+// leaf-step walk, 2 PARK with the speculative walk; + 4: the adaptive tile schedule's launch):
+// out[0..5] = byte offsets of the stack, throughput, hit point, leaf queue, tile descriptors and
+// the block's LDS size; out[6..9] = the first four regions' bytes per lane (entries x element
+// size; they are lane-interleaved with stride kBlock), out[10] = the tile descriptors' bytes
+// (one block-wide region).  tests/test_capi_exports.py checks that the regions are disjoint and
+// inside the block's LDS for every stack size the host can choose.
 extern "C" int rtx_internal_lds_layout(int stack_slots, int park, uint32_t* out) {
+  const bool tiles = (park & 4) != 0;
+  park &= 3;
   if (stack_slots < 1 || stack_slots > 65 || park < 0 || park > 2 || !out) return fail(RTX_ERR_INVALID, "bad argument");
   const bool spec = spec_walk(park, true, false);
-  const PersistLds l = persist_lds(stack_slots, spec);
-  const uint32_t v[9] = {l.stack, l.thr, l.hitp, l.leafq, l.end, (uint32_t)stack_slots * (spec ? 2u : 4u), 24u, 24u,
-                         spec ? kLeafQueue * 4u : 0u};
+  const PersistLds l = persist_lds(stack_slots, spec, tiles);
+  const uint32_t v[11] = {l.stack, l.thr, l.hitp, l.leafq, l.tiles, l.end, (uint32_t)stack_slots * (spec ? 2u : 4u),
+                          24u, 24u, spec ? kLeafQueue * 4u : 0u, tiles ? (uint32_t)sizeof(TileLds) : 0u};
   std::memcpy(out, v, sizeof v);
   return RTX_OK;
 }

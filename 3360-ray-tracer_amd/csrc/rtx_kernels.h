@@ -122,17 +122,83 @@ constexpr size_t stack_lds_bytes(int STACK) { return (size_t)(STACK + 1) * kBloc
 // statement of the layout, used by the kernel and the launch; rtx_internal_lds_layout exposes it
 // to a CPU test that checks the regions are disjoint and inside the block's LDS.
 struct PersistLds {
-  uint32_t stack, thr, hitp, leafq, end;  // byte offsets of the regions in a block's LDS, its size
+  uint32_t stack, thr, hitp, leafq, tiles, end;  // byte offsets of the regions in a block's LDS, its size
 };
+
+// ---------------------------------------------------------------------------------------
+// Adaptive sampling, tile schedule (k_persistent MAP == 2; render_adaptive, rtx_capi.hip).
+// After the uniform first pass (min_spp samples of every pixel, recorded by k_adapt_record),
+// the pixels still sampling are cut into tiles of kTileTP consecutive pixels, ordered within
+// each of the 8 slot regions by their predicted work, largest first.  ONE persistent launch
+// then runs every remaining phase of every tile: a workgroup claims a tile (one atomic per
+// tile), its lanes trace the tile's batch (each pixel's next samples, pixel-major), and once
+// the batch's last path has ended, one wave of the SAME workgroup replays the batch into the
+// pixels' statistics (RecordSample / IsConverged in sample order, lane = pixel) and lays out
+// the tile's next batch in LDS.  A workgroup keeps up to kTileNT tiles in flight, so its lanes
+// trace the other tiles while one waits for its batch's last paths: there is no launch drain
+// between phases, and every hand-off stays inside one CU (LDS counters, workgroup-scope
+// release / acquire), so no cross-XCD visibility is needed.  Largest tiles first keeps the
+// launch's end short: the last tiles claimed are the cheapest.
+// ---------------------------------------------------------------------------------------
+constexpr int kTileTP = 32;  // pixels per tile (the record runs one lane per pixel)
+constexpr int kTileNT = 8;   // tiles in flight per workgroup
+struct PixelSoA {
+  double *sum, *mean, *m2;  // 3 x npix each (channel-major)
+  int32_t* samples;
+  uint8_t* conv;
+};
+// What the tile launch reads (device memory; its address is word 8 * 16 + 6 of the slot
+// counter block, like the slot map's in MAP == 1 launches).
+struct TileArgs {
+  const uint32_t* act;     // subset pixels still sampling after the first pass, in image order
+  const uint32_t* order;   // tile ids (tile t = act[t * kTileTP ...]) in claim order, region by region
+  const uint32_t* rcount;  // tiles of each of the 8 regions
+  const uint32_t* knext;   // each pixel's first batch (k_adapt_record of the first pass)
+  const uint32_t* nact;    // the number of active pixels
+  double* L;               // radiance: kTileTP * kcap slots per (block, descriptor)
+  uint16_t* segs;          // counting builds: each slot's path segments (same indexing), else null
+  unsigned long long* rec_segs;  // counting builds: segments of the recorded samples
+  PixelSoA px;
+  int64_t npix;
+  int32_t kcap;      // largest batch of one pixel
+  int32_t min_spp, budget;
+  int32_t kinc;      // smallest further batch of a pixel not yet converged
+  int32_t max_blocks;  // blocks the radiance workspace has room for
+  int32_t pad_;
+  double rel, margin;
+};
+// A tile in flight (LDS).  word = (cursor << 32) | T: the batch's T slots are claimed by
+// adding to the cursor (an add returns the phase's T with it, so a claim is consistent even
+// when it races the record that starts the next batch); rem counts the batch's paths still
+// running; slot s of the batch is sample s0[i] + (s - off[i]) of pixel pix[i], off[i] <= s <
+// off[i + 1].  state: 0 free, 1 being initialised, 2 in flight.
+struct TileDesc {
+  unsigned long long word;
+  uint32_t rem, state, npx, pad_;
+  uint32_t off[kTileTP + 1];
+  uint32_t pix[kTileTP];
+  uint32_t s0[kTileTP];
+  uint32_t pad2_;
+};
+struct TileLds {
+  uint32_t ready;      // descriptors whose batch has ended (to be recorded)
+  uint32_t exhausted;  // the claim order is used up
+  uint32_t pad_[2];
+  TileDesc d[kTileNT];
+};
+static_assert(sizeof(TileDesc) % 8 == 0 && sizeof(TileLds) % 8 == 0, "8-byte aligned tile descriptors");
+
 // PARK: 0 the plain schedule, 1 the PARK schedule with the leaf-step walk (trace4_run_step),
 // 2 the PARK schedule with the speculative walk (trace4_run_spec; trees of at most
 // kSpecMaxNodes nodes, its stack entries being 16-bit)
 constexpr bool spec_walk(int park, bool fast, bool scatter) { return park == 2 && fast && !scatter; }
 constexpr int64_t kSpecMaxNodes = 65536;
-constexpr PersistLds persist_lds(int stack_slots, bool spec) {
+// tiles: the launch runs the tile schedule (MAP == 2), whose descriptors follow the other regions
+constexpr PersistLds persist_lds(int stack_slots, bool spec, bool tiles = false) {
   const uint32_t stack_bytes = (uint32_t)stack_slots * kBlock * (spec ? 2u : 4u);
-  const uint32_t thr = stack_bytes, hitp = thr + 3u * kBlock * 8u, leafq = hitp + 3u * kBlock * 8u;
-  return PersistLds{0u, thr, hitp, leafq, leafq + (spec ? (uint32_t)kLeafQueue * kBlock * 4u : 0u)};
+  const uint32_t thr = (stack_bytes + 7u) & ~7u, hitp = thr + 3u * kBlock * 8u, leafq = hitp + 3u * kBlock * 8u;
+  const uint32_t tl = leafq + (spec ? (uint32_t)kLeafQueue * kBlock * 4u : 0u);
+  return PersistLds{0u, thr, hitp, leafq, tl, tl + (tiles ? (uint32_t)sizeof(TileLds) : 0u)};
 }
 
 template <int STACK, bool FAST, bool COUNT, int TK = -1>
@@ -296,6 +362,212 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in,
 #endif
 
 // ---------------------------------------------------------------------------------------
+// One pixel's RecordSample (pixel_state.h:22-39) over K radiance records in sample order, each
+// followed by IsConverged (pixel_state.h:54-72), stopping at convergence; the statistics come
+// in and go out through r.  AHEAD: the loads of the next samples kept in flight while the
+// current one is replayed.  Used by k_adapt_record (a kernel of its own) and by the tile
+// schedule's record inside the persistent kernel (fewer loads ahead: registers).
+// ---------------------------------------------------------------------------------------
+struct PixRec {
+  double sum[3], mean[3], m2[3];
+  int n;
+  bool conv;
+};
+template <int AHEAD>
+__device__ __forceinline__ void replay_pixel(PixRec& r, const double* __restrict__ Lp, int K, int min_spp,
+                                             double rel) {
+  auto record = [&](const double (&x)[3]) {
+    r.n++;
+    for (int c = 0; c < 3; c++) {
+      double mu = r.mean[c];
+      double delta = x[c] - mu;
+      mu += delta / r.n;
+      double delta2 = x[c] - mu;
+      r.mean[c] = mu;
+      r.m2[c] += delta2 * delta;
+    }
+    for (int c = 0; c < 3; c++) r.sum[c] += x[c];
+    if (r.n >= min_spp) {
+      // err / mu > rel  <=>  m2 > rel^2 (n - 1) n mu^2 up to the few ulps the exact form rounds
+      // by: decided by products where the two sides differ by more than 1e-10 relative (the
+      // usual case), the exact form (two divisions, two square roots) only in between; NaN
+      // fails both comparisons and takes the exact form too.
+      // (channels in order, the first failing one decides; unrolled, so the statistics stay in
+      // registers)
+      bool ok = true;
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        if (ok) {
+          double mu = fmax(fabs(r.mean[c]), 1e-3);
+          const double thr = rel * rel * ((double)(r.n - 1) * (double)r.n * (mu * mu));
+          if (r.m2[c] > thr * (1.0 + 1e-10)) {
+            ok = false;
+          } else if (!(r.m2[c] < thr * (1.0 - 1e-10))) {
+            double var = r.n > 1 ? r.m2[c] / (r.n - 1) : 0.0;
+            double err = sqrt(var) / sqrt((double)r.n);
+            if (err / mu > rel) ok = false;
+          }
+        }
+      }
+      r.conv = ok;
+    }
+  };
+  double b[AHEAD][3];
+  auto load = [&](int slot, int k) {
+    if (k < K)
+      for (int c = 0; c < 3; c++) b[slot][c] = Lp[3 * k + c];
+  };
+#pragma unroll
+  for (int i = 0; i < AHEAD; i++) load(i, i);
+  for (int k = 0; k < K && !r.conv; k += AHEAD) {
+#pragma unroll
+    for (int i = 0; i < AHEAD; i++) {
+      if (k + i >= K || r.conv) break;
+      record(b[i]);
+      load(i, k + i + AHEAD);
+    }
+  }
+}
+__device__ __forceinline__ void load_pixel(PixRec& r, const PixelSoA& px, int64_t npix, int64_t p) {
+  for (int c = 0; c < 3; c++) r.sum[c] = px.sum[c * npix + p], r.mean[c] = px.mean[c * npix + p], r.m2[c] = px.m2[c * npix + p];
+  r.n = px.samples[p];
+  r.conv = false;
+}
+__device__ __forceinline__ void store_pixel(const PixRec& r, const PixelSoA& px, int64_t npix, int64_t p) {
+  for (int c = 0; c < 3; c++) px.sum[c * npix + p] = r.sum[c], px.mean[c * npix + p] = r.mean[c], px.m2[c * npix + p] = r.m2[c];
+  px.samples[p] = r.n;
+  px.conv[p] = r.conv;
+}
+
+// ---- the tile schedule's pieces (see TileArgs) ----
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(v, o);
+    if ((int)lane_id() >= o) v += t;
+  }
+  return v;
+}
+// A pixel's next batch once its batch is recorded and it is neither converged nor out of
+// budget: IsConverged holds at n samples once n >= var / (rel * max(|mean|, 1e-3))^2 in every
+// channel, so the batch is that many more samples (times the margin), at least kinc, within
+// the budget and the workspace.  Only the amount of work depends on it, never the result: a
+// sample traced past the pixel's convergence point is discarded by the record.
+__device__ __forceinline__ uint32_t tile_next_batch(const PixRec& r, const TileArgs* ta) {
+  const double rel = ta->rel;
+  double need = 0.0;
+  for (int c = 0; c < 3; c++) {
+    const double var = r.n > 1 ? r.m2[c] / (r.n - 1) : 0.0;
+    const double mu = fmax(fabs(r.mean[c]), 1e-3);
+    need = fmax(need, var / (rel * rel * mu * mu));
+  }
+  const int left = ta->budget - r.n;
+  const double want = (need - (double)r.n) * ta->margin;
+  int k = (want < (double)left) ? (int)ceil(want) : left;  // NaN / inf: the whole budget
+  k = max(k, min(ta->kinc, left));
+  return (uint32_t)min(k, min(left, ta->kcap));
+}
+// Slot index of the tile workspace: descriptor j of this block, batch slot s.
+__device__ __forceinline__ uint64_t tile_slot(const TileArgs* ta, int j, uint32_t s) {
+  return ((uint64_t)(blockIdx.x * (uint32_t)kTileNT + (uint32_t)j) * kTileTP) * (uint64_t)ta->kcap + s;
+}
+// Claims a free descriptor and the next tile in claim order (this block's region first, then
+// the others) and lays out the tile's first batch (wave-uniform; the whole wave).  false: no
+// free descriptor, or the claim order is used up (then tl->exhausted is set).
+__device__ __forceinline__ bool tile_claim(TileLds* tl, const TileArgs* ta, unsigned long long* ctr, uint32_t region) {
+  int j = -1;
+  if (lane_id() == 0)
+    for (int q = 0; q < kTileNT; q++)
+      if (atomicCAS(&tl->d[q].state, 0u, 1u) == 0u) {
+        j = q;
+        break;
+      }
+  j = __shfl(j, 0);
+  if (j < 0) return false;
+  int tid = -1;
+  if (lane_id() == 0) {
+    for (int tries = 0; tries < 8 && tid < 0; tries++) {
+      const uint32_t r = (region + tries) & 7;
+      uint32_t base = 0;
+      for (uint32_t q = 0; q < r; q++) base += ta->rcount[q];
+      const uint32_t cnt = ta->rcount[r];
+      if (cnt == 0) continue;
+      const unsigned long long t = atomicAdd(ctr + 16 * r, 1ull);
+      if (t < cnt) tid = (int)ta->order[base + (uint32_t)t];
+    }
+  }
+  tid = __shfl(tid, 0);
+  TileDesc& d = tl->d[j];
+  if (tid < 0) {
+    if (lane_id() == 0) {
+      atomicExch(&tl->exhausted, 1u);
+      atomicExch(&d.state, 0u);
+    }
+    return false;
+  }
+  const uint32_t first = (uint32_t)tid * kTileTP, nact = *ta->nact;
+  const int n = (int)min<uint32_t>(kTileTP, nact - first);
+  const int i = (int)lane_id();
+  uint32_t p = 0, k = 0, s = 0;
+  if (i < n) p = ta->act[first + i], k = ta->knext[p], s = (uint32_t)ta->px.samples[p];
+  const uint32_t inc = wave_incl_scan(k);
+  const uint32_t T = __shfl(inc, 63);
+  if (i < n) d.pix[i] = p, d.s0[i] = s, d.off[i] = inc - k;
+  if (i == 0) d.off[n] = T, d.npx = (uint32_t)n, d.rem = T;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the layout before the claim word
+  if (i == 0) {
+    atomicExch(&d.word, (unsigned long long)T);
+    atomicExch(&d.state, T ? 2u : 0u);  // (an active pixel always has a batch)
+  }
+  return T != 0;
+}
+// The batch of descriptor j has ended: replay it into the pixels' statistics (lane i = pixel
+// i of the tile) and lay out the next batch (wave-uniform; the whole wave).
+template <bool COUNT>
+__device__ __forceinline__ void tile_record(TileLds* tl, const TileArgs* ta, int j) {
+  TileDesc& d = tl->d[j];
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // every lane's radiance store, before its count-off
+  const int i = (int)lane_id();
+  const int n = (int)d.npx;
+  uint32_t kn = 0, nrec = 0;
+  if (i < n) {
+    const uint32_t p = d.pix[i], o0 = d.off[i], K = d.off[i + 1] - o0;
+    PixRec r;
+    load_pixel(r, ta->px, ta->npix, p);
+    const int n0 = r.n;
+    if (K > 0) {
+      const uint64_t base = tile_slot(ta, j, o0);
+      replay_pixel<2>(r, ta->L + 3 * base, (int)K, ta->min_spp, ta->rel);
+      if (COUNT) {  // the segments of the samples recorded (the rest are discarded)
+        unsigned long long t = 0;
+        for (int k = 0; k < r.n - n0; k++) t += ta->segs[base + k];
+        atomicAdd(ta->rec_segs, t);
+      }
+      store_pixel(r, ta->px, ta->npix, p);
+      if (!r.conv && r.n < ta->budget) kn = tile_next_batch(r, ta);
+    }
+    nrec = (uint32_t)r.n;
+  }
+  const uint32_t inc = wave_incl_scan(kn);
+  const uint32_t T = __shfl(inc, 63);
+  if (i < n) d.off[i] = inc - kn, d.s0[i] = nrec;
+  if (i == 0) d.off[n] = T, d.rem = T;
+  // the statistics (global) and the layout (LDS) complete before the next batch is claimable
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (i == 0) {
+    atomicExch(&d.word, (unsigned long long)T);
+    if (T == 0) atomicExch(&d.state, 0u);  // the tile is finished
+  }
+}
+// The wave's exit test: no tile left to claim, none in flight.
+__device__ __forceinline__ bool tiles_done(const TileLds* tl) {
+  bool busy = false;
+#pragma unroll
+  for (int q = 0; q < kTileNT; q++) busy |= ((const volatile uint32_t*)&tl->d[q].state)[0] != 0u;
+  return *(const volatile uint32_t*)&tl->exhausted && !busy && *(const volatile uint32_t*)&tl->ready == 0u;
+}
+
+// ---------------------------------------------------------------------------------------
 // Persistent lanes: each lane owns one path at a time and refills from a global slot
 // counter in wave-sized chunks (one atomic per kChunk slots), so lanes whose path ended
 // (miss, emitter, absorption, Russian roulette) are immediately given a new primary —
@@ -304,22 +576,33 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in,
 // TK >= 0: every primitive in the fast tree has kind TK (the ground sphere is a global
 // primitive, so the bunny's tree holds triangles, the final and mixed scenes' spheres), so
 // the walk's leaf tests are compiled for that kind alone.
-// Which slots the kernel draws: uniform groups (MAP = false), slot p * K + k is sample s0 + k
-// of pixel p; adaptive phases (render_adaptive, MAP = true), slot i is sample smap[i].y of
-// pixel smap[i].x for i below the phase's slot count, where the slot counters' block holds,
-// after the 8 region counters, the slot count (next_slot[128]) and the slot map's address
-// (next_slot[130]), both written by k_adapt_expand.  MAP is a template parameter, not a kernel
-// argument: the fixed-spp kernels run at the SGPR limit, and any extra uniform state there
-// reshuffles their register allocation (a runtime switch cost the bunny's build 3.7 %, r3d).
+// Which slots the kernel draws: uniform groups (MAP = 0), slot p * K + k is sample s0 + k of
+// pixel p; adaptive phases with a slot map (MAP = 1; RTX_FLAG_ADAPT_PHASES), slot i is sample
+// smap[i].y of pixel smap[i].x for i below the phase's slot count, where the slot counters'
+// block holds, after the 8 region counters, the slot count (next_slot[128]) and the slot map's
+// address (next_slot[130]), both written by k_adapt_expand; the adaptive tile schedule (MAP =
+// 2, the default adaptive render after the first pass), slots of the tiles in flight in the
+// block's LDS descriptors (TileArgs at next_slot[134]).  MAP is a template parameter, not a
+// kernel argument: the fixed-spp kernels run at the SGPR limit, and any extra uniform state
+// there reshuffles their register allocation (a runtime switch cost the bunny's build 3.7 %, r3d).
 template <int STACK, bool FAST, bool COUNT, bool SCATTER, int PARK, int TK = -1, bool LAMB = false,
-          bool NOTEX = false, bool NODOF = false, bool MAP = false>
+          bool NOTEX = false, bool NODOF = false, int MAP = 0>
 __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A, unsigned long long* next_slot) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   // the LDS layout (persist_lds: the launch sizes it the same way; the host launches PARK
   // kernels only for fast, non-scatter renders)
   constexpr bool kSpecLds = spec_walk(PARK, FAST, SCATTER);
-  const PersistLds lay = persist_lds(A.stack_slots, kSpecLds);
+  constexpr bool kTiles = MAP == 2;
+  const PersistLds lay = persist_lds(A.stack_slots, kSpecLds, kTiles);
   char* const ldsb = (char*)lds;
+  TileLds* const tl = (TileLds*)(ldsb + lay.tiles);  // (kTiles)
+  const TileArgs* const ta = kTiles ? (const TileArgs*)next_slot[8 * 16 + 6] : nullptr;
+  (void)tl, (void)ta;
+  if (kTiles) {
+    if (blockIdx.x >= (uint32_t)ta->max_blocks) return;  // (the host sizes the grid within it)
+    for (uint32_t w = threadIdx.x; w < sizeof(TileLds) / 4; w += kBlock) ((uint32_t*)tl)[w] = 0u;
+    __syncthreads();
+  }
   uint32_t* stk = (uint32_t*)(ldsb + lay.stack) + threadIdx.x;
   uint16_t* stk16 = (uint16_t*)(ldsb + lay.stack) + threadIdx.x;  // (kSpecLds)
   (void)stk16;
@@ -330,7 +613,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   // nothing else reads rec.p (textured builds: once the texture lookups moved before the sampling)
   constexpr bool kHitpLds = (NOTEX || RTX_EARLY_TEX) && !SCATTER;
   (void)hitp_lds;
-  const uint64_t nslots = MAP ? (uint64_t)next_slot[8 * 16] : (uint64_t)A.npix * (uint64_t)A.K;
+  const uint64_t nslots = MAP == 1 ? (uint64_t)next_slot[8 * 16] : (uint64_t)A.npix * (uint64_t)A.K;
   // GetPixel uses Interval(0.001, inf) (camera.h:158); IntersectBatch uses 0.001f (cpu_ray_integrator.h:21)
   const double tmin = SCATTER ? 0.001 : (double)0.001f;
   Counters c{};
@@ -338,7 +621,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   // counting builds: the lane's path segments, stored per slot when the launch's slot counter
   // block names a buffer for them (adaptive renders: the segments of the recorded samples)
   uint32_t pseg = 0;
-  uint16_t* const segbuf = COUNT ? (uint16_t*)next_slot[8 * 16 + 4] : nullptr;
+  uint16_t* const segbuf = !COUNT ? nullptr : kTiles ? ta->segs : (uint16_t*)next_slot[8 * 16 + 4];
   (void)pseg, (void)segbuf;
   uint64_t chunk_base = 0, chunk_left = 0;  // wave-uniform
   bool exhausted = false;                   // wave-uniform
@@ -357,13 +640,47 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   bool parked = false;
   TravState trs;
   while (true) {
+    if constexpr (kTiles) {  // a tile whose batch has ended is recorded first (at most one per round)
+      const uint32_t rdy = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&tl->ready);
+      if (rdy) {
+        const int j = __builtin_ctz(rdy);
+        uint32_t old = 0;
+        if (lane_id() == 0) old = atomicAnd(&tl->ready, ~(1u << j));
+        old = __builtin_amdgcn_readfirstlane(old);
+        if (old & (1u << j)) tile_record<COUNT>(tl, ta, j);
+      }
+    }
     // ---- refill: ballot of idle lanes, leftover of the current chunk first.  Refilling
     // only once kRefillMin lanes are idle (or the wave is empty) amortises the
     // primary-generation code over several lanes.
     const unsigned long long idle = __ballot(!has);
     bool fresh = false;
     constexpr int kRefill = kPark ? kRefillMinPark : kRefillMin;
-    if (idle != 0 && !exhausted && (__popcll(idle) >= kRefill || idle == ~0ull)) {
+    if (kTiles) {
+      // tile schedule: the idle lanes take slots of the block's tiles in flight (descriptor
+      // order), one LDS add per tile; when those run out, the wave claims the next tile
+      if (idle != 0 && (__popcll(idle) >= kRefill || idle == ~0ull)) {
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+        const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane_id()) - 1ull));
+        uint32_t given = 0;
+        for (int j = 0; j < kTileNT && given < nidle; j++) {
+          const unsigned long long w = *(volatile unsigned long long*)&tl->d[j].word;
+          const uint32_t wc = __builtin_amdgcn_readfirstlane((uint32_t)(w >> 32));
+          const uint32_t wt = __builtin_amdgcn_readfirstlane((uint32_t)w);
+          if (wc >= wt) continue;
+          unsigned long long old = 0;
+          if (lane_id() == 0) old = atomicAdd(&tl->d[j].word, (unsigned long long)(nidle - given) << 32);
+          const uint32_t c0 = __builtin_amdgcn_readfirstlane((uint32_t)(old >> 32));
+          const uint32_t T = __builtin_amdgcn_readfirstlane((uint32_t)old);
+          if (c0 >= T) continue;
+          const uint32_t got = min(nidle - given, T - c0);
+          if (!has && rank >= given && rank < given + got) slot = ((uint32_t)j << 24) | (c0 + rank - given), fresh = true;
+          given += got;
+        }
+        if (given < nidle && !__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&tl->exhausted))
+          tile_claim(tl, ta, next_slot, region);  // its slots go to the next refill
+      }
+    } else if (idle != 0 && !exhausted && (__popcll(idle) >= kRefill || idle == ~0ull)) {
       const uint64_t nidle = (uint64_t)__popcll(idle);
       const uint64_t rank = (uint64_t)__popcll(idle & ((1ull << lane_id()) - 1ull));
       uint64_t cand = ~0ull;
@@ -412,9 +729,20 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
       const RenderArgs& Ar = kArgsAtRefill ? *(const RenderArgs*)kseg : A;
       // nslots < 2^32 (checked on the host): 32-bit division
       uint2 e = make_uint2(0u, 0u);
-      if (MAP) e = ((const uint2*)next_slot[8 * 16 + 2])[slot];
+      if (MAP == 1) e = ((const uint2*)next_slot[8 * 16 + 2])[slot];
+      if (kTiles) {  // batch slot s of descriptor j: the last pixel i with off[i] <= s
+        const TileDesc& d = tl->d[slot >> 24];
+        const uint32_t s = slot & 0xFFFFFFu;
+        int lo = 0, hi = (int)d.npx;
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (d.off[mid] <= s) lo = mid;
+          else hi = mid;
+        }
+        e = make_uint2(d.pix[lo], d.s0[lo] + (s - d.off[lo]));
+      }
       const uint32_t p = MAP ? e.x : (uint32_t)slot / (uint32_t)Ar.K;
-      if (!(Ar.conv && Ar.conv[p])) {
+      if (kTiles || !(Ar.conv && Ar.conv[p])) {  // (a tile slot is always traced: its count-off ends the batch)
         const int k = MAP ? 0 : (int)((uint32_t)slot - p * (uint32_t)Ar.K);
         int x, y;
         Ar.map.xy(p, x, y);
@@ -429,6 +757,11 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
       }
     }
     if (!__any(has)) {
+      if (kTiles) {  // nothing to trace now: leave once no tile is left or in flight, else wait
+        if (__builtin_amdgcn_readfirstlane(tiles_done(tl) ? 1u : 0u)) break;
+        __builtin_amdgcn_s_sleep(2);
+        continue;
+      }
       if (exhausted) break;
       continue;
     }
@@ -508,8 +841,21 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
       }
     }
     if (!cont) {
-      store_radiance(A, slot, L);
-      if (COUNT && segbuf) segbuf[slot] = (uint16_t)min(pseg, 65535u);
+      if (kTiles) {
+        // the radiance record, then the path is counted off its tile's batch; the count-off
+        // that ends the batch marks the tile for its record (by a wave of this block: the
+        // workgroup-scope release orders the store before the LDS count)
+        const int j = (int)(slot >> 24);
+        const uint64_t q = tile_slot(ta, j, slot & 0xFFFFFFu);
+        double* Lq = ta->L + 3 * q;
+        Lq[0] = L.x, Lq[1] = L.y, Lq[2] = L.z;
+        if (COUNT) segbuf[q] = (uint16_t)min(pseg, 65535u);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (atomicSub(&tl->d[j].rem, 1u) == 1u) atomicOr(&tl->ready, 1u << j);
+      } else {
+        store_radiance(A, slot, L);
+        if (COUNT && segbuf) segbuf[slot] = (uint16_t)min(pseg, 65535u);
+      }
       has = false;
     }
   }
@@ -519,19 +865,23 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
 // The PARK instantiations are compiled in their own translation unit (rtx_park.hip), with
 // their own macro defaults (the leaf-step walk, the branchless triangle test) and scheduler
 // options (Makefile PARKFLAGS; the LLVM default since the leaf-step walk, `ab_sch_c3.txt`).
-// (ST: stack size, CO: counting build, SC: scatter API, MP: adaptive slot map, PK: 1 the
-// leaf-step walk, 2 the speculative walk; the host never launches the PARK kernel for the
-// scatter API, nor maps a scatter render's slots, but its dispatch names those builds)
+// (ST: stack size, CO: counting build, SC: scatter API, MP: 0 uniform groups, 1 adaptive slot
+// map, 2 adaptive tiles, PK: 1 the leaf-step walk, 2 the speculative walk; the host never
+// launches the PARK kernel for the scatter API, nor maps a scatter render's slots, but its
+// dispatch names those builds)
 #define RTX_PARK_INSTANCES(X)                                                                                    \
-  X(32, false, false, false, 1) X(32, true, false, false, 1) X(64, false, false, false, 1)                      \
-  X(64, true, false, false, 1) X(32, false, true, false, 1) X(32, true, true, false, 1)                         \
-  X(64, false, true, false, 1) X(64, true, true, false, 1) X(32, false, false, true, 1)                         \
-  X(32, true, false, true, 1) X(64, false, false, true, 1) X(64, true, false, true, 1)                          \
-  X(32, false, false, false, 2) X(32, true, false, false, 2) X(64, false, false, false, 2)                      \
-  X(64, true, false, false, 2) X(32, false, false, true, 2) X(32, true, false, true, 2)                         \
-  X(64, false, false, true, 2) X(64, true, false, true, 2)
-#define RTX_PARK_TRI_INSTANCES(Y) \
-  Y(32, false, 1) Y(64, false, 1) Y(32, true, 1) Y(64, true, 1) Y(32, false, 2) Y(64, false, 2) Y(32, true, 2) Y(64, true, 2)
+  X(32, false, false, 0, 1) X(32, true, false, 0, 1) X(64, false, false, 0, 1)                                  \
+  X(64, true, false, 0, 1) X(32, false, true, 0, 1) X(32, true, true, 0, 1)                                     \
+  X(64, false, true, 0, 1) X(64, true, true, 0, 1) X(32, false, false, 1, 1)                                    \
+  X(32, true, false, 1, 1) X(64, false, false, 1, 1) X(64, true, false, 1, 1)                                   \
+  X(32, false, false, 2, 1) X(32, true, false, 2, 1) X(64, false, false, 2, 1) X(64, true, false, 2, 1)         \
+  X(32, false, false, 0, 2) X(32, true, false, 0, 2) X(64, false, false, 0, 2)                                  \
+  X(64, true, false, 0, 2) X(32, false, false, 1, 2) X(32, true, false, 1, 2)                                   \
+  X(64, false, false, 1, 2) X(64, true, false, 1, 2)                                                            \
+  X(32, false, false, 2, 2) X(32, true, false, 2, 2) X(64, false, false, 2, 2) X(64, true, false, 2, 2)
+#define RTX_PARK_TRI_INSTANCES(Y)                                                                           \
+  Y(32, 0, 1) Y(64, 0, 1) Y(32, 1, 1) Y(64, 1, 1) Y(32, 2, 1) Y(64, 2, 1) Y(32, 0, 2) Y(64, 0, 2) Y(32, 1, 2) \
+      Y(64, 1, 2) Y(32, 2, 2) Y(64, 2, 2)
 #ifndef RTX_PERSISTENT_ONLY
 #define RTX_PARK_EXTERN(ST, CO, SC, MP, PK)                                                                   \
   extern template __global__ void k_persistent<ST, true, CO, SC, PK, -1, false, false, false, MP>(RenderArgs, \
@@ -551,13 +901,8 @@ RTX_PARK_TRI_INSTANCES(RTX_PARK_TRI_EXTERN)
 
 // ---------------------------------------------------------------------------------------
 // RecordSample in sample order (pixel_state.h:22-39) + IsConverged (pixel_state.h:54-72)
+// (PixelSoA: see the tile schedule above)
 // ---------------------------------------------------------------------------------------
-struct PixelSoA {
-  double *sum, *mean, *m2;  // 3 x npix each (channel-major)
-  int32_t* samples;
-  uint8_t* conv;
-};
-
 #ifndef RTX_PERSISTENT_ONLY  // rtx_park.hip: the persistent kernel's PARK instantiations only
 __global__ __launch_bounds__(kBlock) void k_accumulate(PixelSoA px, const double* __restrict__ L, int64_t npix,
                                                        int K, int adaptive, int min_spp, double rel) {
@@ -660,67 +1005,18 @@ __global__ __launch_bounds__(kBlock) void k_adapt_record(PixelSoA px, const doub
   uint32_t kn = 0;
   if (K > 0 && !px.conv[p]) {
     const double* __restrict__ Lp = L + 3 * (ap.off ? (int64_t)ap.off[q] : p * (int64_t)ap.kuni);
-    double sum[3], mean[3], m2[3];
-    for (int c = 0; c < 3; c++) sum[c] = px.sum[c * npix + p], mean[c] = px.mean[c * npix + p], m2[c] = px.m2[c * npix + p];
-    int n = px.samples[p];
-    bool conv = false;
-    // RecordSample (pixel_state.h:22-39), then IsConverged (pixel_state.h:54-72)
-    auto record = [&](const double (&x)[3]) {
-      n++;
-      for (int c = 0; c < 3; c++) {
-        double mu = mean[c];
-        double delta = x[c] - mu;
-        mu += delta / n;
-        double delta2 = x[c] - mu;
-        mean[c] = mu;
-        m2[c] += delta2 * delta;
-      }
-      for (int c = 0; c < 3; c++) sum[c] += x[c];
-      if (n >= ap.min_spp) {
-        // err / mu > rel  <=>  m2 > rel^2 (n - 1) n mu^2 up to the few ulps the exact form rounds
-        // by: decided by products where the two sides differ by more than 1e-10 relative (the
-        // usual case), the exact form (two divisions, two square roots) only in between; NaN
-        // fails both comparisons and takes the exact form too.
-        bool ok = true;
-        for (int c = 0; c < 3 && ok; c++) {
-          double mu = fmax(fabs(mean[c]), 1e-3);
-          const double thr = ap.rel * ap.rel * ((double)(n - 1) * (double)n * (mu * mu));
-          if (m2[c] > thr * (1.0 + 1e-10)) {
-            ok = false;
-          } else if (!(m2[c] < thr * (1.0 - 1e-10))) {
-            double var = n > 1 ? m2[c] / (n - 1) : 0.0;
-            double err = sqrt(var) / sqrt((double)n);
-            if (err / mu > ap.rel) ok = false;
-          }
-        }
-        conv = ok;
-      }
-    };
-    double b[kRecAhead][3];
-    auto load = [&](int slot, int k) {
-      if (k < K)
-        for (int c = 0; c < 3; c++) b[slot][c] = Lp[3 * k + c];
-    };
-#pragma unroll
-    for (int i = 0; i < kRecAhead; i++) load(i, i);
-    for (int k = 0; k < K && !conv; k += kRecAhead) {
-#pragma unroll
-      for (int i = 0; i < kRecAhead; i++) {
-        if (k + i >= K || conv) break;
-        record(b[i]);
-        load(i, k + i + kRecAhead);
-      }
-    }
+    PixRec r;
+    load_pixel(r, px, npix, p);
+    const int n0 = r.n;
+    replay_pixel<kRecAhead>(r, Lp, K, ap.min_spp, ap.rel);
     if (ap.segs) {  // counting render: the segments of the samples recorded (the rest are discarded)
       const uint16_t* sg = ap.segs + (ap.off ? (int64_t)ap.off[q] : p * (int64_t)ap.kuni);
       unsigned long long t = 0;
-      for (int k = 0; k < n - px.samples[p]; k++) t += sg[k];
+      for (int k = 0; k < r.n - n0; k++) t += sg[k];
       atomicAdd(ap.rec_segs, t);
     }
-    for (int c = 0; c < 3; c++) px.sum[c * npix + p] = sum[c], px.mean[c * npix + p] = mean[c], px.m2[c * npix + p] = m2[c];
-    px.samples[p] = n;
-    px.conv[p] = conv;
-    if (!conv && n < ap.budget) kn = adapt_next_batch(mean, m2, n, ap);
+    store_pixel(r, px, npix, p);
+    if (!r.conv && r.n < ap.budget) kn = adapt_next_batch(r.mean, r.m2, r.n, ap);
   }
   ap.knext[q] = kn;
   const unsigned long long na = __popcll(__ballot(kn != 0));
@@ -784,6 +1080,50 @@ __global__ __launch_bounds__(kBlock) void k_adapt_expand(const uint32_t* __restr
     }
     smap[i] = make_uint2(s_p[lo], s_s0[lo] + (i - s_off[lo]));
   }
+}
+
+// ---- the tile schedule's claim order (render_adaptive): the pixels still sampling after the
+// first pass, compacted in image order (flag, exclusive scan, compact), cut into tiles of
+// kTileTP, each keyed by (region, predicted work descending) for a radix sort, so each region's
+// tiles are claimed largest batch first.  The region of a tile is the 1/8 band of the subset's
+// pixels its first pixel lies in: the same bands the first pass's slot regions cover, so a
+// block keeps to its XCD group's band of the image as long as the band has tiles.
+__global__ __launch_bounds__(kBlock) void k_tile_flags(const uint32_t* __restrict__ knext, int64_t npix,
+                                                       uint32_t* __restrict__ flag) {
+  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (p < npix) flag[p] = knext[p] != 0u ? 1u : 0u;
+}
+__global__ __launch_bounds__(kBlock) void k_tile_compact(const uint32_t* __restrict__ flag,
+                                                         const uint32_t* __restrict__ idx, int64_t npix,
+                                                         uint32_t* __restrict__ act, uint32_t* __restrict__ nact) {
+  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (p >= npix) return;
+  if (flag[p]) act[idx[p]] = (uint32_t)p;
+  if (p == npix - 1) *nact = idx[p] + flag[p];
+}
+__global__ __launch_bounds__(kBlock) void k_tile_keys(const uint32_t* __restrict__ act,
+                                                      const uint32_t* __restrict__ nact,
+                                                      const uint32_t* __restrict__ knext, int64_t npix,
+                                                      int64_t max_tiles, uint32_t* __restrict__ keys,
+                                                      uint32_t* __restrict__ vals, uint32_t* __restrict__ rcount) {
+  const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (t >= max_tiles) return;
+  const int64_t first = t * kTileTP, na = *nact;
+  vals[t] = (uint32_t)t;
+  if (first >= na) {
+    keys[t] = 0xFFFFFFFFu;  // no such tile: sorted after every region
+    return;
+  }
+  uint32_t work = 0;
+  for (int64_t i = first; i < min<int64_t>(first + kTileTP, na); i++) work += knext[act[i]];
+  const uint32_t region = (uint32_t)min<int64_t>(7, ((int64_t)act[first] * 8) / max<int64_t>(1, npix));
+  keys[t] = (region << 24) | (0xFFFFFFu - min(work, 0xFFFFFFu));
+  atomicAdd(&rcount[region], 1u);
+}
+// The launch's TileArgs into device memory, its address into the slot counter block.
+__global__ void k_tile_setup(TileArgs a, TileArgs* __restrict__ dst, unsigned long long* __restrict__ ctr) {
+  *dst = a;
+  ctr[8 * 16 + 6] = (unsigned long long)dst;
 }
 #endif
 

@@ -19,6 +19,8 @@ RTX_SEAM_TMIN = float(np.float32(0.001))
 MODES = {"wavefront": 0, "persistent": 1, "megakernel": 2}
 PRECISIONS = {"parity": 0, "fast": 1}
 RTX_FLAG_COUNT, RTX_FLAG_PARK, RTX_FLAG_NO_PARK, RTX_FLAG_GENERIC, RTX_FLAG_LEAF_STEP = 1, 2, 4, 8, 16
+# adaptive persistent renders: round 3's one-launch-per-phase schedule instead of the tile schedule
+RTX_FLAG_ADAPT_PHASES = 32
 # "park": the PARK schedule with its default walk (speculative on trees of at most 65536 nodes);
 # "park_step": the PARK schedule with the leaf-step walk on every tree
 SCHEDULE_FLAGS = {None: 0, "auto": 0, "park": RTX_FLAG_PARK, "park_step": RTX_FLAG_PARK | RTX_FLAG_LEAF_STEP,
@@ -291,13 +293,14 @@ class DeviceScene:
 
     def render(self, cam, spp, max_depth, seed=1234, adaptive=True, mode="wavefront", precision="parity",
                tile=None, stripes=None, samples_per_group=0, min_spp=16, rel_threshold=float(np.float32(0.05)),
-               count=False, schedule=None, generic=False):
+               count=False, schedule=None, generic=False, adapt_phases=False):
         p = RenderParams()
         p.spp, p.max_depth, p.adaptive = spp, max_depth, int(bool(adaptive))
         p.min_spp, p.rel_threshold, p.seed = min_spp, rel_threshold, seed
         p.mode, p.precision = MODES[mode], PRECISIONS[precision]
         p.samples_per_group = samples_per_group
-        p.flags = (1 if count else 0) | SCHEDULE_FLAGS[schedule] | (RTX_FLAG_GENERIC if generic else 0)
+        p.flags = ((1 if count else 0) | SCHEDULE_FLAGS[schedule] | (RTX_FLAG_GENERIC if generic else 0)
+                   | (RTX_FLAG_ADAPT_PHASES if adapt_phases else 0))
         if stripes is not None:
             p.stripe_rows, p.stripe_index, p.stripe_count = stripes
         elif tile is not None:
@@ -345,6 +348,16 @@ class DeviceScene:
                                        C.c_void_p(d_spp) if d_spp else None, C.byref(st) if stats else None,
                                        C.c_void_p(stream) if stream else None), "rtx_render_device")
         return st.as_dict() if stats else None
+
+
+def adapt_tune(tile_kcap=0, tile_kinc=0, tile_margin=0.0, phase_slots=0, phase_kcap=0):
+    """Test / tuning hook (rtx_internal_adapt_tune, not in rtx.h): overrides of the adaptive
+    schedules' constants for the renders that follow in this process; no argument (all 0)
+    restores the defaults.  Results never depend on them, only the work and the phases do."""
+    f = lib().rtx_internal_adapt_tune
+    f.argtypes = [C.c_int32, C.c_int32, C.c_double, C.c_int64, C.c_int32]
+    f.restype = C.c_int
+    _check(f(tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap), "rtx_internal_adapt_tune")
 
 
 def render_multi(scenes, cam, spp, max_depth, seed=1234, adaptive=True, mode="persistent", precision="fast",

@@ -126,6 +126,9 @@ def main():
     ap.add_argument("--adaptive", action="store_true",
                     help="the reference's default sampling (wavefront.cc:42-43, 62-69, 125-127): per-pixel "
                          "adaptive, at least 16 samples, relative error 0.05f, up to the workload's spp")
+    ap.add_argument("--adapt-schedule", default="tiles", choices=["tiles", "phases"],
+                    help="adaptive renders after the first pass: tiles in one launch (default) or one launch per "
+                         "phase (round 3's schedule; RTX_FLAG_ADAPT_PHASES)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-generic-leg", action="store_true", help="skip the generic-build comparison frames")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -161,7 +164,8 @@ def main():
     dev = rtx.DeviceScene(host, device=dev_id)
     cam = rtx.camera(rtx.camera_config(preset, width=width))
     W, H = cam.image_width, cam.image_height
-    sched_flags = rtx.SCHEDULE_FLAGS[args.schedule] | (rtx.RTX_FLAG_GENERIC if args.generic else 0)
+    sched_flags = (rtx.SCHEDULE_FLAGS[args.schedule] | (rtx.RTX_FLAG_GENERIC if args.generic else 0)
+                   | (rtx.RTX_FLAG_ADAPT_PHASES if args.adapt_schedule == "phases" else 0))
 
     def params(flags=sched_flags, generic=False):
         p = rtx.RenderParams()

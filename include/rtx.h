@@ -41,9 +41,10 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 6  /* 2: rtx_stats.node_bytes; 3: rtx_stats.parked, RTX_FLAG_PARK / NO_PARK;
+#define RTX_ABI_VERSION 7  /* 2: rtx_stats.node_bytes; 3: rtx_stats.parked, RTX_FLAG_PARK / NO_PARK;
                               4: rtx_stats.build, RTX_FLAG_GENERIC, rtx_render_multi;
-                              5: RTX_FLAG_LEAF_STEP, RTX_BUILD_SPECULATIVE; 6: rtx_stats.rays_recorded */
+                              5: RTX_FLAG_LEAF_STEP, RTX_BUILD_SPECULATIVE; 6: rtx_stats.rays_recorded;
+                              7: RTX_FLAG_ADAPT_PHASES (the adaptive tile schedule is the default) */
 
 enum {
   RTX_OK = 0,
@@ -208,7 +209,11 @@ enum {
   /* the PARK schedule's traversal: the speculative walk (queued leaf tests) by default on
      trees of at most 65536 BVH4 nodes, the leaf-step walk on larger ones; this flag asks for
      the leaf-step walk on every tree (same results) */
-  RTX_FLAG_LEAF_STEP = 16
+  RTX_FLAG_LEAF_STEP = 16,
+  /* RTX_MODE_PERSISTENT adaptive renders (samples_per_group 0): after the first pass, the
+     further passes run in tiles of pixels inside one launch (default); this flag asks for the
+     earlier schedule, one launch per phase with a device-wide slot map (same results) */
+  RTX_FLAG_ADAPT_PHASES = 32
 };
 
 /* rtx_stats.build: which persistent-kernel build ran (the per-scene specialisations compile

@@ -481,6 +481,10 @@ std::vector<T> read_bin(const std::string& path) {
 void render_wavefront(RefScene& S, Cam& cam, int max_depth, int max_spp, int batch, bool adaptive,
                       const std::string& out) {
   integrator::CPURayIntegrator integ(&S.world);
+  // REF_PAR_SHADE=1 (timing only: scripts/calibrate_cpu.py): the shading loop runs in parallel as
+  // the reference runs it; otherwise serially, the draw order fixed by SeedRng (the goldens)
+  const char* pe = std::getenv("REF_PAR_SHADE");
+  const bool par_shade = pe && std::atoi(pe) != 0;
   const float kRelThresh = 0.05;
   const int kMinSamples = adaptive ? 16 : (1 << 30);
   const int W = cam.image_width, H = cam.image_height, N = W * H;
@@ -514,7 +518,8 @@ void render_wavefront(RefScene& S, Cam& cam, int max_depth, int max_spp, int bat
         std::vector<geom::HitRecord> hits;
         integ.IntersectBatch(br, hits);
         rays += (long long)cnt;
-        for (size_t i = 0; i < cnt; ++i) {
+        // one ray's shading (wavefront.cc:109-208); `push` takes a continuing child
+        auto shade = [&](size_t i, std::vector<integrator::RayState>& push) {
           auto rs = q[off + i];
           auto& ps = px[rs.pixel_index];
           const auto& rec = hits[i];
@@ -523,13 +528,13 @@ void render_wavefront(RefScene& S, Cam& cam, int max_depth, int max_spp, int bat
           if (!rec.hit || rs.depth >= max_depth) {
             L += rs.throughput * sky(r);
             finish(ps, L);
-            continue;
+            return;
           }
           Color em = rec.mat->Emitted(rec.u, rec.v, rec.p);
           if (!em.NearZero()) {
             L += rs.throughput * em;
             finish(ps, L);
-            continue;
+            return;
           }
           Vec3 wo = -core::Normalize(r.direction());
           Vec3 wi;
@@ -537,9 +542,9 @@ void render_wavefront(RefScene& S, Cam& cam, int max_depth, int max_spp, int bat
           Color f;
           if (!rec.mat->Sample(rec, wo, wi, pdf, f)) {
             finish(ps, L);
-            continue;
+            return;
           }
-          if (ps.converged) continue;
+          if (ps.converged) return;
           integrator::RayState child;
           child.r = core::Ray(rec.p, wi);
           child.pixel_index = rs.pixel_index;
@@ -549,7 +554,7 @@ void render_wavefront(RefScene& S, Cam& cam, int max_depth, int max_spp, int bat
           } else {
             if (pdf < 1e-6f) {
               finish(ps, L);
-              continue;
+              return;
             }
             float cos_theta = std::max(0.0f, static_cast<float>(core::Dot(wi, rec.normal)));
             child.throughput = rs.throughput * f * cos_theta / pdf;
@@ -559,11 +564,25 @@ void render_wavefront(RefScene& S, Cam& cam, int max_depth, int max_spp, int bat
             p = std::clamp(p, 0.1, 0.95);
             if (core::RandomDouble() > p) {
               finish(ps, L);
-              continue;
+              return;
             }
             child.throughput /= p;
           }
-          nq.push_back(child);
+          push.push_back(child);
+        };
+        if (par_shade) {
+          // the reference's own schedule (wavefront.cc:105-217): the shading loop under
+          // `omp parallel for schedule(dynamic)`, children in thread-local queues merged in
+          // thread order (a pixel has at most one ray in flight per pass, so its PixelState is
+          // touched by one thread at a time); each thread draws from its own thread_local
+          // generator (core/random.h), so the draw order, and the image, are not reproducible
+          const int nt = omp_get_max_threads();
+          std::vector<std::vector<integrator::RayState>> local(nt);
+#pragma omp parallel for schedule(dynamic)
+          for (int i = 0; i < (int)cnt; i++) shade((size_t)i, local[omp_get_thread_num()]);
+          for (int t = 0; t < nt; t++) nq.insert(nq.end(), local[t].begin(), local[t].end());
+        } else {
+          for (size_t i = 0; i < cnt; ++i) shade(i, nq);
         }
         off += cnt;
       }
@@ -595,6 +614,7 @@ void render_wavefront(RefScene& S, Cam& cam, int max_depth, int max_spp, int bat
   st << "loop_seconds " << std::chrono::duration<double>(t_loop - t_start).count() << "\n";
   st << "render_seconds " << std::chrono::duration<double>(t_end - t_start).count() << "\n";
   st << "threads " << omp_get_max_threads() << "\n";
+  st << "parallel_shading " << (par_shade ? 1 : 0) << "\n";
 }
 
 // Megakernel mode (mega_kernel.h:15-54 + DefaultSampler sampler.h:22-34 + GetPixel

@@ -4,7 +4,7 @@ container from the reference's sources by oracle/Makefile; it travels to the GPU
 
 Times the reference's own renderer (oracle/_ref/ref_harness: the reference's CPURayIntegrator,
 materials and PixelState driven by the Render() glue of wavefront.cc:40-242; its OpenMP
-IntersectBatch on REF_THREADS threads) and the CPU restatement used as bench.py's
+IntersectBatch and, as the reference runs it, its OpenMP shading loop on REF_THREADS threads) and the CPU restatement used as bench.py's
 cpu_baseline (oracle/librtx_oracle.so, per-pixel Philox mode, OpenMP) on identical
 configurations and the same number of threads, fixed spp.  The ratio port/reference
 calibrates bench.py's cpu_baseline against the reference.
@@ -45,12 +45,21 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "cpu_calibration.json"))
     ap.add_argument("--host", default=f"build container, {os.cpu_count()} CPUs")
+    ap.add_argument("--serial-shading", action="store_true",
+                    help="run the reference's shading loop serially (round 3's calibration); by default it runs "
+                         "in parallel as wavefront.cc:105-217 does (omp parallel for schedule(dynamic), thread-local "
+                         "child queues merged in thread order)")
     args = ap.parse_args()
     import gen_golden
     import oracle_ctypes as orc
     import rtx
 
-    out = {"threads": args.threads, "host": args.host, "cases": {}}
+    out = {"threads": args.threads, "host": args.host, "cases": {},
+           "reference_parallel": ("IntersectBatch (cpu_ray_integrator.h:24) only" if args.serial_shading else
+                                  "IntersectBatch (cpu_ray_integrator.h:24) and the shading loop (wavefront.cc:105-217, "
+                                  "schedule(dynamic), thread-local child queues)"),
+           "reference_serial": "primary generation (wavefront.cc:62-79), batch copies and queue merges, as in the "
+                               "reference"}
     with tempfile.TemporaryDirectory() as td:
         for name, scene, preset, width, spp, depth in CASES:
             if args.only and name not in args.only.split(","):
@@ -58,12 +67,13 @@ def main():
             path = os.path.join(td, scene + ".rtxs")
             rtx.HostScene.recipe(scene, 1234).write(path)
             cfg = orc.camera_preset(preset)
-            env = dict(os.environ, REF_THREADS=str(args.threads))
+            env = dict(os.environ, REF_THREADS=str(args.threads), REF_PAR_SHADE="0" if args.serial_shading else "1")
             prefix = os.path.join(td, name)
             subprocess.run([str(a) for a in [HARNESS, "render", path, MODELS, *gen_golden.cam_args(cfg, width), depth, spp, 0, 1234,
                             prefix]], check=True, env=env, cwd=MODELS)  # (image textures by file name)
             st = dict(l.split() for l in open(prefix + ".stats"))
             ref_rays, ref_s = int(st["rays"]), float(st["loop_seconds"])
+            assert int(st.get("parallel_shading", "0")) == (0 if args.serial_shading else 1)
             s = orc.Scene(path)
             t0 = time.perf_counter()
             _, _, pst = s.render(cfg, width, spp, depth, 1234, adaptive=0, rng="philox", mode="per_pixel",

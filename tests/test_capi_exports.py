@@ -29,7 +29,7 @@ def test_every_declared_symbol_is_exported(rtx_mod):
 
 
 def test_abi_version(rtx_mod):
-    assert rtx_mod.lib().rtx_abi_version() == 6
+    assert rtx_mod.lib().rtx_abi_version() == 7
 
 
 def test_library_is_a_gfx950_code_object(rtx_mod):
@@ -59,7 +59,7 @@ def test_invalid_descriptors_rejected_before_launch(rtx_mod):
     assert rc == -1 and b"material out of range" in rtx_mod.lib().rtx_last_error()
 
 
-@pytest.mark.parametrize("park", [0, 1, 2])
+@pytest.mark.parametrize("park", [0, 1, 2, 4, 5, 6])
 def test_persistent_lds_regions_are_disjoint(rtx_mod, park):
     """The persistent kernel's LDS regions (traversal stacks, throughput, hit point, leaf queue)
     are each lane-interleaved with their own element size, so a byte shared by two regions
@@ -67,17 +67,23 @@ def test_persistent_lds_regions_are_disjoint(rtx_mod, park):
     6-word leaf queue laid over the hit-point words faulted exactly that way (ledger,
     cmp_spec6_fault.txt).  The layout the kernel and the launch share (persist_lds, exported as a
     host-only test hook) must keep every region inside the block's LDS and apart from the others,
-    for every stack size the host can choose (the lean walk's exact bound + 1, up to 65)."""
+    for every stack size the host can choose (the lean walk's exact bound + 1, up to 65), with and
+    without the adaptive tile schedule's descriptors (park + 4), a block-wide region after them."""
     f = rtx_mod.lib().rtx_internal_lds_layout
     f.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_uint32)]
-    out = (C.c_uint32 * 9)()
+    out = (C.c_uint32 * 11)()
+    spec, tiles = (park & 3) == 2, bool(park & 4)
     for slots in range(1, 66):
         assert f(slots, park, out) == 0
-        stack, thr, hitp, leafq, end, *per_lane = list(out)
-        assert (per_lane[3] != 0) == (park == 2) and per_lane[0] == slots * (2 if park == 2 else 4)
-        regions = [(o, o + 256 * b) for o, b in zip((stack, thr, hitp, leafq), per_lane) if b]
+        stack, thr, hitp, leafq, tl, end, *per_lane = list(out)
+        assert (per_lane[3] != 0) == spec and per_lane[0] == slots * (2 if spec else 4)
+        assert (per_lane[4] != 0) == tiles
+        regions = [(o, o + 256 * b) for o, b in zip((stack, thr, hitp, leafq), per_lane[:4]) if b]
+        if tiles:
+            regions.append((tl, tl + per_lane[4]))
         regions.sort()
         assert regions[0][0] == 0 and regions[-1][1] == end, (slots, regions, end)
         for (a0, a1), (b0, b1) in zip(regions, regions[1:]):
             assert a1 <= b0, (slots, regions)
-        assert thr % 8 == 0 and hitp % 8 == 0 and end <= 160 * 1024, (slots, thr, hitp, end)  # a workgroup may take all 160 KiB
+        assert thr % 8 == 0 and hitp % 8 == 0 and tl % 8 == 0, (slots, thr, hitp, tl)
+        assert end <= 160 * 1024, (slots, end)  # a workgroup may take all 160 KiB

@@ -229,22 +229,34 @@ def test_group_size_does_not_change_results(rtx_mod, dev_scenes):
                                                                ("bunny", "c3_bunny", 400, 64, 20, "park"),
                                                                ("cornell", "cornell", 300, 48, 20, "plain"),
                                                                ("three", "c1_three", 64, 24, 4, None)])
-def test_adaptive_phases_equal_uniform_groups(rtx_mod, dev_scenes, scene, preset, w, spp, depth, schedule):
+def test_adaptive_schedules_equal_uniform_groups(rtx_mod, dev_scenes, scene, preset, w, spp, depth, schedule):
     # (the Cornell box is too noisy for any pixel to converge within 48 samples: every pixel
-    # takes the whole budget through the phases' growing batches)
-    """Adaptive persistent renders run in phases (render_adaptive: per-pixel batch sizes
-    predicted from each pixel's statistics, slot maps, two interleaved sub-renders on two
-    streams from 2^16 pixels up): the same pixels and sample counts, bit for bit, as uniform
-    groups of 4 samples over every pixel."""
+    # takes the whole budget through the growing batches)
+    """Adaptive persistent renders predict each pixel's batches from its statistics: the tile
+    schedule (default: after a uniform first pass, one launch runs every further batch of tiles
+    of pixels, each recorded inside its workgroup), the same with forced tiny batches (many
+    phases per tile: largest batch 4 / 3 samples, smallest 1, margin 0.5) and the phase
+    schedule (RTX_FLAG_ADAPT_PHASES: one launch per phase over a device-wide slot map, also with
+    a forced small workspace and phase floor).  Each gives the same pixels and sample counts,
+    bit for bit, as uniform groups of 4 samples over every pixel."""
     cam = rtx_mod.camera(rtx_mod.camera_config(preset, width=w))
     d = dev_scenes(scene)
     kw = dict(seed=17, adaptive=True, mode="persistent", precision="fast", schedule=schedule)
-    a, sa, sta = d.render(cam, spp, depth, **kw)
     b, sb, stb = d.render(cam, spp, depth, samples_per_group=4, **kw)
-    assert np.array_equal(sa, sb), np.nonzero(sa != sb)[0][:5]
-    assert np.array_equal(a, b)
-    assert sa.min() >= min(16, spp) and sa.max() <= spp and ((sa < spp).any() or scene == "cornell")
-    assert sta["rays_primary"] >= sa.sum() and stb["rays_primary"] >= sa.sum()
+    assert sb.min() >= min(16, spp) and sb.max() <= spp and ((sb < spp).any() or scene == "cornell")
+    runs = [("tiles", {}, {}), ("tiles_kcap4", dict(tile_kcap=4, tile_kinc=1, tile_margin=0.5), {}),
+            ("tiles_kcap3", dict(tile_kcap=3, tile_kinc=2, tile_margin=2.0), {}),
+            ("phases", {}, dict(adapt_phases=True)),
+            ("phases_small", dict(phase_slots=1024, phase_kcap=8), dict(adapt_phases=True))]
+    try:
+        for name, tune, extra in runs:
+            rtx_mod.adapt_tune(**tune)
+            a, sa, sta = d.render(cam, spp, depth, **kw, **extra)
+            assert np.array_equal(sa, sb), (name, np.nonzero(sa != sb)[0][:5])
+            assert np.array_equal(a, b), name
+            assert sta["rays_primary"] >= sa.sum(), name
+    finally:
+        rtx_mod.adapt_tune()
 
 
 def test_edge_cases(rtx_mod, dev_scenes, tmp_path, gpu):

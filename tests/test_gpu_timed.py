@@ -133,8 +133,8 @@ def test_timed_kernel_builds_adaptive_match_oracle(rtx_mod, orc, scenes, acase, 
 def test_adaptive_recorded_segments_equal_oracle(rtx_mod, orc, scenes, acase, rows):
     """The counting build's rays_recorded (the segments of the samples the pixels record; the
     adaptive bench line's value counts only these) equals the oracle's segment count exactly, and
-    the samples traced past convergence are the difference to rays_total.  70 full-width rows are
-    >= 2^16 pixels, so the render runs as two interleaved sub-renders."""
+    the samples traced past convergence are the difference to rays_total (2 and 70 full-width
+    rows: a few to thousands of tiles)."""
     ci, spp, _ = acase
     scene, preset, width, _, depth, _, _ = BENCH_CASES[ci]
     path, d = scenes(scene)
@@ -149,6 +149,44 @@ def test_adaptive_recorded_segments_equal_oracle(rtx_mod, orc, scenes, acase, ro
     _, _, fst = d.render(cam, 4, depth, seed=515, adaptive=False, mode="persistent", precision="fast", tile=tile,
                          count=True)
     assert fst["rays_recorded"] == fst["rays_total"] > 0  # fixed spp: every sample is recorded
+
+
+# The configurations' own budgets through FORCED small workspaces (rtx_internal_adapt_tune):
+# the paths only a large frame at a large budget reaches on its own — a pixel's batches capped
+# (tile kcap, phase kcap / workspace), the phase floor few remaining pixels get, many phases —
+# compared with the oracle on sample counts, recorded segments and pixels.
+FULL_BUDGET_CASES = [(1, 200, 0.7), (3, 2048, 0.5)]  # bench case index, spp, band row (fraction of H)
+TUNES = {"tiles": ({}, False), "tiles_small": (dict(tile_kcap=8, tile_kinc=4, tile_margin=0.75), False),
+         "tiles_one": (dict(tile_kcap=1, tile_kinc=1), False), "phases": ({}, True),
+         "phases_small": (dict(phase_slots=4096, phase_kcap=8), True)}
+
+
+@pytest.mark.parametrize("tune", sorted(TUNES))
+@pytest.mark.parametrize("fcase", FULL_BUDGET_CASES, ids=[f"{BENCH_CASES[c[0]][1]}_{c[1]}spp" for c in FULL_BUDGET_CASES])
+def test_adaptive_full_budget_small_workspace_matches_oracle(rtx_mod, orc, scenes, fcase, tune):
+    """One full-width row at the configuration's whole budget (C3 200 spp, C5 2048 spp), with
+    the workspace and floors forced small: identical per-pixel sample counts, recorded segments
+    equal to the oracle's, RMS <= RMS_TOL."""
+    ci, spp, yfrac = fcase
+    scene, preset, width, _, depth, _, _ = BENCH_CASES[ci]
+    path, d = scenes(scene)
+    cam = rtx_mod.camera(rtx_mod.camera_config(preset, width=width))
+    tile = (0, int(cam.image_height * yfrac), cam.image_width, 1)
+    ref, ref_spp, ref_st = oracle(orc, path, preset, width, spp, depth, 616, tile, adaptive=1)
+    knobs, phases = TUNES[tune]
+    try:
+        rtx_mod.adapt_tune(**knobs)
+        rgb, sp, st = d.render(cam, spp, depth, seed=616, adaptive=True, mode="persistent", precision="fast",
+                               tile=tile, count=True, min_spp=ADAPTIVE_MIN, rel_threshold=ADAPTIVE_REL,
+                               adapt_phases=phases)
+    finally:
+        rtx_mod.adapt_tune()
+    ref_spp = ref_spp.ravel()
+    assert ref_spp.max() > 64  # the row reaches deep into the budget
+    assert np.array_equal(sp, ref_spp), (np.nonzero(sp != ref_spp)[0][:5], sp[sp != ref_spp][:5])
+    assert st["rays_recorded"] == ref_st["rays"], (st["rays_recorded"], ref_st["rays"], st["rays_total"])
+    rms = np.sqrt(np.mean((rgb - ref.reshape(-1, 3)) ** 2))
+    assert rms <= RMS_TOL, rms
 
 
 @pytest.mark.parametrize("case", BENCH_CASES, ids=[c[1] for c in BENCH_CASES])
