@@ -724,9 +724,17 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
       // SGPRs 79 -> 60, scratch 52 -> 0 B), so they keep the arguments in registers;
       // profiles/r03/ab_kernarg_refill_r4g_*).
       constexpr bool kArgsAtRefill = !(LAMB && NOTEX);
+      // RTX_CAM_KARG (A/B): those builds read only the camera from the argument segment
+      constexpr bool kCamAtRefill = kArgsAtRefill || RTX_CAM_KARG;
       auto kseg = __builtin_amdgcn_kernarg_segment_ptr();
-      if (kArgsAtRefill) asm volatile("" : "+s"(kseg));
+      if (kCamAtRefill) asm volatile("" : "+s"(kseg));
       const RenderArgs& Ar = kArgsAtRefill ? *(const RenderArgs*)kseg : A;
+      const rtx_camera& Cr = kCamAtRefill ? ((const RenderArgs*)kseg)->cam : A.cam;
+      // (A must stay the kernel's first parameter: the counting builds, which every parity
+      // test of the counts and the bench's counting pass run, check the argument segment
+      // against the arguments and fault on a mismatch)
+      if (COUNT && kArgsAtRefill && (Ar.npix != A.npix || Ar.seed != A.seed || Ar.stack_slots != A.stack_slots))
+        __builtin_trap();
       // nslots < 2^32 (checked on the host): 32-bit division
       uint2 e = make_uint2(0u, 0u);
       if (MAP == 1) e = ((const uint2*)next_slot[8 * 16 + 2])[slot];
@@ -748,7 +756,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
         Ar.map.xy(p, x, y);
         pix = (uint32_t)(y * Ar.map.W + x), smp = MAP ? e.y : (uint32_t)(Ar.s0 + k);
         Rng g = make_rng(A.seed, pix, smp, 0u);
-        get_ray<NODOF>(Ar.cam, x, y, g, P.o, P.d);
+        get_ray<NODOF>(Cr, x, y, g, P.o, P.d);
         thr_lds[0] = 1.0, thr_lds[kBlock] = 1.0, thr_lds[2 * kBlock] = 1.0;
         P.depth = SCATTER ? Ar.max_depth : 0;
         has = true;

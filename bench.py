@@ -130,6 +130,8 @@ def main():
                     help="adaptive renders after the first pass: tiles in one launch (default) or one launch per "
                          "phase (round 3's schedule; RTX_FLAG_ADAPT_PHASES)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-adaptive-leg", action="store_true",
+                    help="skip the adaptive-sampling frames timed beside a fixed-spp line")
     ap.add_argument("--no-generic-leg", action="store_true", help="skip the generic-build comparison frames")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--dist-backend", default="gloo",
@@ -137,6 +139,10 @@ def main():
                          "collective touches the data path, so the host-side group the 1-GPU rehearsals run is "
                          "the one an 8-GPU run takes) or nccl (= RCCL)")
     args = ap.parse_args()
+    if args.adaptive and args.mode != "persistent":
+        # the metric counts the segments of the recorded samples, which the counting build
+        # reports for the persistent kernel's adaptive schedules only (rtx_stats.rays_recorded)
+        ap.error("--adaptive needs --mode persistent")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -167,9 +173,10 @@ def main():
     sched_flags = (rtx.SCHEDULE_FLAGS[args.schedule] | (rtx.RTX_FLAG_GENERIC if args.generic else 0)
                    | (rtx.RTX_FLAG_ADAPT_PHASES if args.adapt_schedule == "phases" else 0))
 
-    def params(flags=sched_flags, generic=False):
+    def params(flags=sched_flags, generic=False, adaptive=None):
         p = rtx.RenderParams()
-        p.spp, p.max_depth, p.adaptive, p.seed = spp, depth, int(args.adaptive), args.seed
+        p.spp, p.max_depth, p.seed = spp, depth, args.seed
+        p.adaptive = int(args.adaptive if adaptive is None else adaptive)
         p.min_spp, p.rel_threshold = ADAPTIVE_MIN_SPP, ADAPTIVE_REL
         p.mode, p.precision = rtx.MODES[args.mode], rtx.PRECISIONS[args.precision]
         p.stripe_rows, p.stripe_index, p.stripe_count = STRIPE_ROWS, rank, world
@@ -287,6 +294,12 @@ def main():
                        "steps": g_steps, "build": rtx.build_names(gst[-1]["build"]),
                        "note": "same frame with RTX_FLAG_GENERIC: no per-scene specialisation (same pixels)"}
 
+    # the reference's default sampling (adaptive, WavefrontRenderer::Render) on the same frame,
+    # timed beside the fixed-spp line so the driver's run measures it too
+    adaptive_leg = None
+    if world == 1 and not args.adaptive and not args.no_adaptive_leg and args.mode == "persistent":
+        adaptive_leg = time_adaptive(torch, step, params, per_frame, rays_all / elapsed / 1e6)
+
     out = None
     if rank == 0:
         out = {
@@ -325,6 +338,8 @@ def main():
             out["rays_recorded_per_step"] = recorded / steps
         if generic_leg:
             out["generic_build"] = generic_leg
+        if adaptive_leg:
+            out["adaptive"] = adaptive_leg
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"], out["rms_vs_cpu"], out["rms_check"] = cpu_baseline(
                 rtx, dev, host, cam, preset, scene_name, spp, depth, args, parked, build_bits)
@@ -332,12 +347,85 @@ def main():
             if args.adaptive and rc["rows"] == [0, H]:  # the CPU rendered the whole frame
                 rc["segments_gpu_recorded"] = int(cst["rays_recorded"])
                 rc["recorded_segments_identical"] = int(cst["rays_recorded"]) == rc["segments_cpu"]
+            if adaptive_leg:
+                adaptive_leg.update(cpu_check_adaptive(rtx, dev, host, cam, preset, spp, depth, args,
+                                                       adaptive_leg.pop("_recorded_whole")))
     frame.close(rank, dist)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def time_adaptive(torch, step, params, per_frame_fixed, fixed_value):
+    """The same frame with the reference's default sampling (adaptive: at least 16 samples,
+    relative error 0.05f, up to the workload's spp; wavefront.cc:42-43, 62-69, 125-127), ~2.5 s
+    of frames.  value counts the segments of the samples the pixels record (the counting pass's
+    rays_recorded: the same frame, deterministic); traced_value adds the samples traced past a
+    pixel's convergence and discarded."""
+    ap = params(adaptive=True)
+    t = time.perf_counter()
+    step(ap)  # first adaptive frame: workspace allocation
+    step(ap)
+    per = (time.perf_counter() - t) / 2
+    n = max(3, min(200, int(2.5 / max(per, 1e-4))))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sts = [step(ap) for _ in range(n)]
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    cst = step(params(ap.flags | 1, adaptive=True))  # RTX_FLAG_COUNT
+    rec, traced = cst["rays_recorded"], sum(s["rays_total"] for s in sts) / n
+    hot_ms = sum(s["hot_kernel_ms"] for s in sts) / n
+    return {"metric": "Mrays/s of the recorded samples' segments, adaptive sampling (the reference's default)",
+            "value": rec * n / el / 1e6, "traced_value": traced * n / el / 1e6, "unit": "Mrays/s",
+            "ms_per_step": el * 1e3 / n, "steps": n, "hot_kernel_ms_per_step": hot_ms,
+            "hot_launches_per_step": sts[-1]["hot_launches"],
+            "rays_recorded_per_step": rec, "rays_traced_per_step": traced,
+            "recorded_fraction_of_traced": rec / max(1.0, traced), "vs_fixed_spp_value": rec * n / el / 1e6 / fixed_value,
+            "schedule": "phases" if ap.flags & 32 else "tiles",
+            "sampling": sampling_text(True), "_recorded_whole": rec}
+
+
+def cpu_check_adaptive(rtx, dev, host, cam, preset, spp, depth, args, recorded_whole):
+    """The adaptive frame on the CPU oracle (whole frame when it takes under ~25 s on this host,
+    else a centred band) against the GPU's render of the same pixels: sample counts, recorded
+    segments (counting build) and RMS."""
+    import tempfile
+
+    import oracle_ctypes as orc
+
+    threads = args.cpu_threads or available_cpus()
+    W, H = cam.image_width, cam.image_height
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "scene.rtxs")
+        host.write(path)
+        s = orc.Scene(path)
+        cfg = orc.camera_preset(preset)
+        kw = dict(adaptive=1, rng="philox", mode="per_pixel", threads=threads)
+        t0 = time.perf_counter()
+        s.render(cfg, W, spp, depth, args.seed, tile=(0, H // 2 - 2, W, 4), **kw)
+        per_row = (time.perf_counter() - t0) / 4
+        ch = int(max(4, min(H, 25.0 / max(per_row, 1e-6))))
+        tile = (0, max(0, H // 2 - ch // 2), W, ch)
+        t0 = time.perf_counter()
+        ref, ref_spp, st = s.render(cfg, W, spp, depth, args.seed, tile=tile, **kw)
+        dt = time.perf_counter() - t0
+    gpu, gpu_spp, gst = dev.render(cam, spp, depth, seed=args.seed, adaptive=True, tile=tile, mode="persistent",
+                                   precision=args.precision, count=True, min_spp=ADAPTIVE_MIN_SPP,
+                                   rel_threshold=ADAPTIVE_REL)
+    whole = ch == H
+    return {"rms_vs_cpu": float(np.sqrt(np.mean((gpu - ref.reshape(-1, 3)) ** 2))),
+            "rms_check": {"rows": [tile[1], tile[1] + tile[3]],
+                          "sample_counts_identical": bool(np.array_equal(gpu_spp, ref_spp.ravel())),
+                          "segments_cpu": int(st["rays"]), "segments_gpu_recorded": int(gst["rays_recorded"]),
+                          "recorded_segments_identical": int(gst["rays_recorded"]) == int(st["rays"]),
+                          "whole_frame_recorded_identical": (int(recorded_whole) == int(st["rays"])) if whole else None,
+                          "mean_spp": float(np.mean(ref_spp)), "pixels_converged_early": float(np.mean(ref_spp < spp))},
+            "cpu_baseline": {"value": st["rays"] / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+                             "sample": f"{'the whole' if whole else f'centre band {W}x{ch} of the same'} {W}x{H} frame, "
+                                       f"adaptive, {st['rays']} segments in {dt:.1f}s (oracle/rtx_oracle.cc, philox)"}}
 
 
 def sampling_text(adaptive):

@@ -247,9 +247,12 @@ typedef struct {
   uint64_t sphere_tests;
   uint64_t parked;          /* 1: the persistent fast schedule that parks long traversals ran */
   uint64_t build;           /* RTX_BUILD_* bits of the persistent kernel build (0: wavefront mode) */
-  uint64_t rays_recorded;   /* with RTX_FLAG_COUNT: segments of the samples the pixels recorded (adaptive
-                               sampling traces some samples past a pixel's convergence and discards them;
-                               = rays_total otherwise); 0 without RTX_FLAG_COUNT */
+  uint64_t rays_recorded;   /* with RTX_FLAG_COUNT: segments of the samples the pixels recorded.  Fixed spp:
+                               = rays_total.  Adaptive RTX_MODE_PERSISTENT renders with automatic grouping
+                               (samples_per_group 0; the tile or phase schedule) trace some samples past a
+                               pixel's convergence and discard them: counted per sample.  Other adaptive
+                               renders (wavefront, megakernel, explicit samples_per_group): 0 (not
+                               counted).  0 without RTX_FLAG_COUNT */
 } rtx_stats;
 
 /* ---- entry points ------------------------------------------------------------------ */
