@@ -114,6 +114,7 @@ constexpr double kAdaptMarginStep = 0.25;      // render_adaptive: batch margin 
 constexpr int kTileKcap = 128;
 constexpr int kTileKinc = 8;
 constexpr double kTileMargin = 1.0;
+constexpr bool kTileFirstPassInLaunch = false;  // the first pass inside the tile launch (else a uniform launch of its own)
 // Overrides of the adaptive schedules' constants (0: the default): rtx_internal_adapt_tune, a
 // test and tuning hook (not in rtx.h) that forces small workspaces and floors, so the paths
 // that only a large frame at a large budget reaches run on small frames too.
@@ -122,6 +123,7 @@ struct AdaptTune {
   double tile_margin;
   int64_t phase_slots;  // phases: the smallest phase planned while pixels remain (kAdaptPhaseSlots)
   int phase_kcap;       // phases: the largest batch of one pixel (else from the workspace)
+  int tile_first_pass;  // tiles: 1 the first pass in the tile launch too, 2 in a launch of its own (0: default)
 };
 static AdaptTune g_tune{};
 struct AdaptWs {
@@ -362,6 +364,60 @@ int build_fast4(const rtx_bvh_node* n, const rtx_prim* prims, std::vector<F4Node
     }
   }
   return need;
+}
+
+// RTX_QNODE: each F4Node quantised into one 64-byte QNode (rtx_device.h): per axis the origin is
+// the smallest live lower plane and the step the smallest power of two with 254 steps covering
+// the planes; every lower plane byte is the largest q with fmaf(q, s, o) <= the f32 plane and
+// every upper one the smallest q with fmaf(q, s, o) >= it, the device's own decode (one
+// rounding), so the decoded box contains the f32 box.  false: a non-finite plane.
+static bool quantise_f4(const std::vector<F4Node>& f4, std::vector<QNode>& out) {
+  out.assign(f4.size(), QNode{});
+  for (size_t i = 0; i < f4.size(); i++) {
+    const F4Node& f = f4[i];
+    QNode& q = out[i];
+    for (int c = 0; c < 4; c++) q.child[c] = f.child[c];
+    const float* lo[3] = {f.lox, f.loy, f.loz};
+    const float* hi[3] = {f.hix, f.hiy, f.hiz};
+    for (int a = 0; a < 3; a++) {
+      float mn = INFINITY, mx = -INFINITY;
+      for (int c = 0; c < 4; c++)
+        if (lo[a][c] <= hi[a][c]) mn = std::min(mn, lo[a][c]), mx = std::max(mx, hi[a][c]);
+      q.qlo[a] = 0xFFFFFFFFu, q.qhi[a] = 0u;  // every slot empty until set
+      if (mn > mx) {  // no live slot
+        q.o[a] = 0.0f, q.s[a] = 1.0f;
+        continue;
+      }
+      if (!std::isfinite(mn) || !std::isfinite(mx)) return false;
+      const double ext = (double)mx - (double)mn;
+      int e = ext > 0 ? std::ilogb(ext / 254.0) : -126;
+      e = std::max(-126, e);
+      for (;; e++) {
+        if (e > 127) return false;
+        const float st = std::ldexp(1.0f, e);
+        bool ok = true;
+        uint32_t wl = 0, wh = 0;
+        for (int c = 0; c < 4 && ok; c++) {
+          uint32_t bl = 255u, bh = 0u;
+          if (lo[a][c] <= hi[a][c]) {
+            int ql = (int)std::floor(((double)lo[a][c] - mn) / st);
+            ql = std::max(0, std::min(255, ql));
+            while (ql > 0 && std::fmaf((float)ql, st, mn) > lo[a][c]) ql--;
+            int qh = (int)std::ceil(((double)hi[a][c] - mn) / st);
+            qh = std::max(0, std::min(255, qh));
+            while (qh < 255 && std::fmaf((float)qh, st, mn) < hi[a][c]) qh++;
+            ok = std::fmaf((float)ql, st, mn) <= lo[a][c] && std::fmaf((float)qh, st, mn) >= hi[a][c];
+            bl = (uint32_t)ql, bh = (uint32_t)qh;
+          }
+          wl |= bl << (8 * c), wh |= bh << (8 * c);
+        }
+        if (!ok) continue;
+        q.o[a] = mn, q.s[a] = st, q.qlo[a] = wl, q.qhi[a] = wh;
+        break;
+      }
+    }
+  }
+  return true;
 }
 
 // Fast-path tree of our own: binned SAH on all three axes (32 bins)
@@ -833,6 +889,36 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     }
     return RTX_OK;
   };
+  // the first pass inside the tile launch: tiles of every pixel in image order, each starting
+  // with min_spp samples per pixel (no uniform launch, no record kernel, no claim-order sort)
+  const bool one_launch = tiles && (g_tune.tile_first_pass ? g_tune.tile_first_pass == 1 : kTileFirstPassInLaunch);
+  if (one_launch) {
+    RenderArgs Ag = A;
+    Ag.L = w.lbuf.as<double>(), Ag.conv = nullptr, Ag.K = 1, Ag.s0 = 0;
+    RegionCounts rcn{};
+    const int64_t nt = max_tiles;
+    for (int r = 0; r < 8; r++) {  // tile t's region: min(7, kTileTP * t * 8 / npix)
+      auto first_tile = [&](int64_t q) { return std::min<int64_t>(nt, (q * npix + 8 * kTileTP - 1) / (8 * kTileTP)); };
+      rcn.c[r] = (uint32_t)((r == 7 ? nt : first_tile(r + 1)) - first_tile(r));
+    }
+    TileArgs ta{};
+    ta.act = nullptr, ta.order = nullptr, ta.rcount = w.tcount.as<uint32_t>(), ta.knext = nullptr;
+    ta.nact = w.tcount.as<uint32_t>() + 8;
+    ta.L = w.lbuf.as<double>();
+    ta.segs = L.count ? w.segs.as<uint16_t>() : nullptr;
+    ta.rec_segs = A.counters + 9;
+    ta.px = px, ta.npix = npix;
+    ta.kcap = kcap, ta.min_spp = prm->min_spp, ta.budget = budget, ta.kinc = tile_kinc;
+    ta.max_blocks = (int32_t)max_blocks, ta.k1 = std::min(K1, kcap);  // (a batch never exceeds kcap)
+    ta.rel = prm->rel_threshold, ta.margin = tile_margin;
+    hipLaunchKernelGGL(k_tile_setup, dim3(1), dim3(1), 0, s, ta, w.targs.as<TileArgs>(), ctr, rcn, (uint32_t)npix,
+                       w.tcount.as<uint32_t>());
+    HIPC(hipGetLastError());
+    Launch Lg = L;
+    Lg.map = 2;
+    Lg.max_grid = (int)max_blocks;
+    return launch(1, Lg, Ag, nullptr, npix);
+  }
   // phase 1: min_spp samples of every pixel, one uniform launch over the whole render (the
   // scene's radiance buffer)
   if ((rc = sc->lbuf.reserve((size_t)npix * K1 * 3 * sizeof(double)))) return rc;
@@ -876,9 +962,10 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ta.rec_segs = A.counters + 9;
     ta.px = px, ta.npix = npix;
     ta.kcap = kcap, ta.min_spp = prm->min_spp, ta.budget = budget, ta.kinc = tile_kinc;
-    ta.max_blocks = (int32_t)max_blocks;
+    ta.max_blocks = (int32_t)max_blocks, ta.k1 = K1;
     ta.rel = prm->rel_threshold, ta.margin = tile_margin;
-    hipLaunchKernelGGL(k_tile_setup, dim3(1), dim3(1), 0, s, ta, w.targs.as<TileArgs>(), ctr);
+    hipLaunchKernelGGL(k_tile_setup, dim3(1), dim3(1), 0, s, ta, w.targs.as<TileArgs>(), ctr, RegionCounts{},
+                       (uint32_t)npix, w.tcount.as<uint32_t>());
     HIPC(hipGetLastError());
     Lg.map = 2;
     Lg.max_grid = (int)max_blocks;
@@ -1062,7 +1149,13 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
       sc->stack_fast = need < 0 ? -1 : (need <= 32 ? 32 : (need <= 64 ? 64 : -1));
       sc->fast_need = need;
       sc->n_f4 = f4.size();
+#if RTX_QNODE
+      std::vector<QNode> qn;
+      if (!quantise_f4(f4, qn)) sc->stack_fast = -1;  // (no fast path: the parity walk serves the scene)
+      if (sc->stack_fast > 0 && (rc = upload(sc->fnodes, qn.data(), qn.size(), s))) return rc;
+#else
       if (sc->stack_fast > 0 && (rc = upload(sc->fnodes, f4.data(), f4.size(), s))) return rc;
+#endif
       sc->fast_ok = sc->stack_fast > 0;
     }
   }
@@ -1074,7 +1167,7 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
   S.mats = sc->mats.as<rtx_material>();
   S.texs = sc->texs.as<rtx_texture>();
   S.images = sc->images.as<DImage>();
-  S.f4nodes = (f4.empty() || !sc->fast_ok) ? nullptr : sc->fnodes.as<F4Node>();
+  S.f4nodes = (f4.empty() || !sc->fast_ok) ? nullptr : sc->fnodes.as<FastNode>();
   S.use_bvh = (d->nodes && d->n_nodes > 0) ? 1 : 0;
   S.n_prims = S.use_bvh ? d->n_prims : d->n_prims;
   S.froot_leaf = 0, S.froot_count = 0;
@@ -1476,7 +1569,7 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     stats->tri_tests = h[6];
     stats->sphere_tests = h[7];
     stats->build = prm->mode == RTX_MODE_WAVEFRONT ? 0 : L.build;
-    stats->node_bytes = L.fast ? sizeof(F4Node) : sizeof(rtx_bvh_node);
+    stats->node_bytes = L.fast ? sizeof(F4Node) : sizeof(rtx_bvh_node);  // (the byte model's 4 x 32 B boxes; a QNode is 64 B)
     // segments of the recorded samples: counted per slot by the counting build in adaptive
     // phases (k_adapt_record); every sample is recorded at fixed spp; unknown otherwise
     stats->rays_recorded = !L.count ? 0 : phased ? h[9] : (prm->adaptive ? 0 : h[0]);
@@ -1803,10 +1896,11 @@ extern "C" int rtx_internal_check_sincos(int device, int64_t n, uint64_t seed, i
 // largest batch.  Results never depend on them, only the amount of work and the number of
 // phases do (tests/test_gpu_timed.py runs the full budgets through forced small workspaces).
 extern "C" int rtx_internal_adapt_tune(int32_t tile_kcap, int32_t tile_kinc, double tile_margin, int64_t phase_slots,
-                                       int32_t phase_kcap) {
-  if (tile_kcap < 0 || tile_kinc < 0 || !(tile_margin >= 0) || phase_slots < 0 || phase_kcap < 0)
-    return fail(RTX_ERR_INVALID, "negative tuning value");
-  g_tune = AdaptTune{tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap};
+                                       int32_t phase_kcap, int32_t tile_first_pass) {
+  if (tile_kcap < 0 || tile_kinc < 0 || !(tile_margin >= 0) || phase_slots < 0 || phase_kcap < 0 ||
+      tile_first_pass < 0 || tile_first_pass > 2)
+    return fail(RTX_ERR_INVALID, "bad tuning value");
+  g_tune = AdaptTune{tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap, tile_first_pass};
   return RTX_OK;
 }
 

@@ -237,13 +237,35 @@ struct F4Node {
 };
 static_assert(sizeof(F4Node) == 128, "F4Node must be two 64-byte lines");
 
+// RTX_QNODE (A/B): the same 4-wide nodes quantised into one 64-byte line.  Per axis a, the
+// node's f32 origin o[a] and a power-of-two step s[a]; per child and axis, the entry and exit
+// planes as bytes q: plane = fma(q, s, o), an exact product rounded once.  The host
+// (quantise_f4, rtx_capi.hip) picks each q so that the decoded plane lies outside the F4Node's
+// outward-rounded f32 plane (checked with the same fmaf), so a decoded box contains the f32
+// box and the slab test on it stays conservative with the same argument as on the f32 box.
+// Empty slots: lo bytes 255, hi bytes 0 (an inverted box).
+struct QNode {
+  float o[3], s[3];
+  int32_t child[4];
+  uint32_t qlo[3], qhi[3];  // axis a: byte c = child slot c's plane
+};
+static_assert(sizeof(QNode) == 64, "QNode must be one 64-byte line");
+#ifndef RTX_QNODE
+#define RTX_QNODE 0
+#endif
+#if RTX_QNODE
+typedef QNode FastNode;
+#else
+typedef F4Node FastNode;
+#endif
+
 struct DScene {
   const rtx_bvh_node* nodes;  // parity layout, reference pre-order
   const rtx_prim* prims;      // leaf order
   const rtx_material* mats;
   const rtx_texture* texs;
   const DImage* images;
-  const F4Node* f4nodes;  // 4-wide fast layout (root at 0) or nullptr
+  const FastNode* f4nodes;  // 4-wide fast layout (root at 0) or nullptr
   int64_t n_prims;
   int32_t use_bvh;
   int32_t froot_leaf;  // fast BVH: the whole tree is one leaf (count in froot_count)
@@ -746,6 +768,9 @@ __device__ __forceinline__ FRay4L make_fray4l(V3 o, V3 d) {
   fray4_axis_signed(o.x, d.x, 0, b.ix, b.nlx, b.nhx, b.ox);
   fray4_axis_signed(o.y, d.y, 1, b.iy, b.nly, b.nhy, b.oy);
   fray4_axis_signed(o.z, d.z, 2, b.iz, b.nlz, b.nhz, b.oz);
+#if RTX_QNODE  // entry-plane word of axis a: qlo[a] (byte 40 + 4a) for inv >= 0, else qhi[a] (52 + 4a)
+  b.ox = b.ox & 16u ? 52u : 40u, b.oy = b.oy & 16u ? 56u : 44u, b.oz = b.oz & 16u ? 60u : 48u;
+#endif
   constexpr float lo = 0.99999f, hi = 1.00001f;
   FRay4L r;
   r.iex = b.ix * lo, r.iey = b.iy * lo, r.iez = b.iz * lo;
@@ -800,6 +825,38 @@ __device__ __forceinline__ void trav_globals(const DScene& S, V3 o, V3 d, double
 // Pieces of a lean BVH4 node visit shared by trace4_run and trace4_run_step.
 // The slab tests of node `node`'s four slots: entry distances of the internal children entered
 // (+inf otherwise) in tt, the child words in cc; returns the mask of leaf slots entered.
+#if RTX_QNODE
+__device__ __forceinline__ uint32_t visit_slabs(const char* __restrict__ nbase, uint32_t node, const FRay4L& r,
+                                                float tmax_x, float (&tt)[4], int32_t (&cc)[4]) {
+  const uint32_t noff = node << 6;  // sizeof(QNode) == 64
+  const uint4 w0 = *(const uint4*)(nbase + noff), w1 = *(const uint4*)(nbase + (noff + 16u));
+  const uint4 w2 = *(const uint4*)(nbase + (noff + 32u)), w3 = *(const uint4*)(nbase + (noff + 48u));
+  const uint32_t wv[16] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x, w2.y, w2.z, w2.w, w3.x, w3.y, w3.z, w3.w};
+  const float ox = __uint_as_float(wv[0]), oy = __uint_as_float(wv[1]), oz = __uint_as_float(wv[2]);
+  const float sx = __uint_as_float(wv[3]), sy = __uint_as_float(wv[4]), sz = __uint_as_float(wv[5]);
+  cc[0] = (int32_t)wv[6], cc[1] = (int32_t)wv[7], cc[2] = (int32_t)wv[8], cc[3] = (int32_t)wv[9];
+  // entry / exit plane words by the ray's signs (qlo at words 10..12, qhi at 13..15)
+  const uint32_t ex = r.ox == 40u ? wv[10] : wv[13], fx = r.ox == 40u ? wv[13] : wv[10];
+  const uint32_t ey = r.oy == 44u ? wv[11] : wv[14], fy = r.oy == 44u ? wv[14] : wv[11];
+  const uint32_t ez = r.oz == 48u ? wv[12] : wv[15], fz = r.oz == 48u ? wv[15] : wv[12];
+  auto dq = [](uint32_t w, int c, float s, float o) {  // the decoded plane (exact product, one rounding)
+    const float q = (float)((w >> (8 * c)) & 0xFFu);  // (v_cvt_f32_ubyte<c>)
+    return fmaf(q, s, o);
+  };
+  uint32_t lmask = 0;
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    const float tn = fmaxf(fmaxf(fmaf(dq(ex, c, sx, ox), r.iex, r.nex), fmaf(dq(ey, c, sy, oy), r.iey, r.ney)),
+                           fmaxf(fmaf(dq(ez, c, sz, oz), r.iez, r.nez), 0.0f));
+    const float tf = fminf(fminf(fmaf(dq(fx, c, sx, ox), r.ixx, r.nxx), fmaf(dq(fy, c, sy, oy), r.ixy, r.nxy)),
+                           fminf(fmaf(dq(fz, c, sz, oz), r.ixz, r.nxz), tmax_x));
+    const bool hit = tn <= tf;
+    lmask |= (hit && cc[c] < 0) ? (1u << c) : 0u;
+    tt[c] = (hit && cc[c] >= 0) ? tn : __builtin_inff();
+  }
+  return lmask;
+}
+#else
 __device__ __forceinline__ uint32_t visit_slabs(const char* __restrict__ nbase, uint32_t node, const FRay4L& r,
                                                 float tmax_x, float (&tt)[4], int32_t (&cc)[4]) {
   const uint32_t noff = node << 7;  // sizeof(F4Node) == 128
@@ -821,6 +878,7 @@ __device__ __forceinline__ uint32_t visit_slabs(const char* __restrict__ nbase, 
   }
   return lmask;
 }
+#endif
 // The primitive of leaf slot c (its child word holds ~index)
 __device__ __forceinline__ uint32_t leaf_prim(const int32_t (&cc)[4], int c) {
   const int32_t c01 = (c & 1) ? cc[1] : cc[0], c23 = (c & 1) ? cc[3] : cc[2];

@@ -164,7 +164,8 @@ struct TileArgs {
   int32_t min_spp, budget;
   int32_t kinc;      // smallest further batch of a pixel not yet converged
   int32_t max_blocks;  // blocks the radiance workspace has room for
-  int32_t pad_;
+  int32_t k1;          // act == nullptr: the launch runs the first pass too (every pixel, tiles in
+                       // image order, first batch k1 = min_spp samples; order and knext unused)
   double rel, margin;
 };
 // A tile in flight (LDS).  word = (cursor << 32) | T: the batch's T slots are claimed by
@@ -493,7 +494,7 @@ __device__ __forceinline__ bool tile_claim(TileLds* tl, const TileArgs* ta, unsi
       const uint32_t cnt = ta->rcount[r];
       if (cnt == 0) continue;
       const unsigned long long t = atomicAdd(ctr + 16 * r, 1ull);
-      if (t < cnt) tid = (int)ta->order[base + (uint32_t)t];
+      if (t < cnt) tid = ta->act ? (int)ta->order[base + (uint32_t)t] : (int)(base + (uint32_t)t);
     }
   }
   tid = __shfl(tid, 0);
@@ -509,7 +510,11 @@ __device__ __forceinline__ bool tile_claim(TileLds* tl, const TileArgs* ta, unsi
   const int n = (int)min<uint32_t>(kTileTP, nact - first);
   const int i = (int)lane_id();
   uint32_t p = 0, k = 0, s = 0;
-  if (i < n) p = ta->act[first + i], k = ta->knext[p], s = (uint32_t)ta->px.samples[p];
+  if (i < n) {
+    if (ta->act) p = ta->act[first + i], k = ta->knext[p];
+    else p = first + (uint32_t)i, k = (uint32_t)ta->k1;
+    s = (uint32_t)ta->px.samples[p];
+  }
   const uint32_t inc = wave_incl_scan(k);
   const uint32_t T = __shfl(inc, 63);
   if (i < n) d.pix[i] = p, d.s0[i] = s, d.off[i] = inc - k;
@@ -1128,8 +1133,18 @@ __global__ __launch_bounds__(kBlock) void k_tile_keys(const uint32_t* __restrict
   keys[t] = (region << 24) | (0xFFFFFFu - min(work, 0xFFFFFFu));
   atomicAdd(&rcount[region], 1u);
 }
-// The launch's TileArgs into device memory, its address into the slot counter block.
-__global__ void k_tile_setup(TileArgs a, TileArgs* __restrict__ dst, unsigned long long* __restrict__ ctr) {
+// The launch's TileArgs into device memory, its address into the slot counter block; with the
+// first pass in the launch (a.act == nullptr), also the tile counts of the regions and the
+// pixel count (tiles of every pixel in image order: rcount_fp, nact_fp).
+struct RegionCounts {
+  uint32_t c[8];
+};
+__global__ void k_tile_setup(TileArgs a, TileArgs* __restrict__ dst, unsigned long long* __restrict__ ctr,
+                             RegionCounts rc, uint32_t npix_fp, uint32_t* __restrict__ tcount) {
+  if (!a.act) {
+    for (int r = 0; r < 8; r++) tcount[r] = rc.c[r];
+    tcount[8] = npix_fp;
+  }
   *dst = a;
   ctr[8 * 16 + 6] = (unsigned long long)dst;
 }

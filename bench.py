@@ -129,6 +129,9 @@ def main():
     ap.add_argument("--adapt-schedule", default="tiles", choices=["tiles", "phases"],
                     help="adaptive renders after the first pass: tiles in one launch (default) or one launch per "
                          "phase (round 3's schedule; RTX_FLAG_ADAPT_PHASES)")
+    ap.add_argument("--adapt-tune", default="",
+                    help="tuning of the adaptive schedules (rtx.adapt_tune), e.g. tile_first_pass=1,tile_kcap=64 "
+                         "(never changes results, only the work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-adaptive-leg", action="store_true",
                     help="skip the adaptive-sampling frames timed beside a fixed-spp line")
@@ -163,6 +166,9 @@ def main():
 
     import rtx
 
+    if args.adapt_tune:
+        kv = dict(x.split("=") for x in args.adapt_tune.split(","))
+        rtx.adapt_tune(**{k: (float(v) if k == "tile_margin" else int(v)) for k, v in kv.items()})
     workload = args.workload if args.workload != "auto" else ("c3_bunny" if world == 1 else "c4_bunny4k")
     scene_name, preset, width, spp, depth = WORKLOADS[workload]
     spp = args.spp or spp

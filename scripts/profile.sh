@@ -9,7 +9,7 @@ OUT="$R/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp || exit 1
-B="--no-cpu-baseline --no-generic-leg"
+B="--no-cpu-baseline --no-generic-leg --no-adaptive-leg"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- python3 "$R/bench.py" $B "$@" > "$OUT/bench_trace.json" 2> "$OUT/trace.err" || exit $?
 for c in FETCH_SIZE WRITE_SIZE \
          "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \

@@ -13,8 +13,7 @@ timeout -k 10 120 python bench.py --adaptive --adapt-schedule phases --steps 10 
 RTX_DEBUG_ADAPT=1 timeout -k 10 120 python bench.py --adaptive --steps 1 --warmup 1 --no-cpu-baseline --no-generic-leg > $O/dbg_tiles.json 2> $O/dbg_tiles.err || exit 1
 RTX_DEBUG_ADAPT=1 timeout -k 10 120 python bench.py --adaptive --adapt-schedule phases --steps 1 --warmup 1 --no-cpu-baseline --no-generic-leg > $O/dbg_phases.json 2> $O/dbg_phases.err || exit 1
 
-# the camera-only argument refill of the bunny's Lambertian texture-free builds (round 3's
-# unmeasured r4n), fixed spp and adaptive
-timeout -k 10 600 bash scripts/ab.sh r5a_camkarg_c3 "--no-generic-leg" default 3360-ray-tracer_amd/variants/librtx_camkarg.so > /dev/null || exit 1
-timeout -k 10 600 bash scripts/ab.sh r5a_camkarg_c3a "--no-generic-leg --adaptive" default 3360-ray-tracer_amd/variants/librtx_camkarg.so > /dev/null || exit 1
+echo done
+timeout -k 10 120 python bench.py --adaptive --adapt-tune tile_first_pass=1 --steps 10 --warmup 2 --no-cpu-baseline --no-generic-leg > $O/bench_c3a_tiles1.json 2> $O/bench_c3a_tiles1.err || exit 1
+RTX_DEBUG_ADAPT=1 timeout -k 10 120 python bench.py --adaptive --adapt-tune tile_first_pass=1 --steps 1 --warmup 1 --no-cpu-baseline --no-generic-leg > $O/dbg_tiles1.json 2> $O/dbg_tiles1.err || exit 1
 echo done2

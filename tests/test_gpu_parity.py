@@ -244,7 +244,10 @@ def test_adaptive_schedules_equal_uniform_groups(rtx_mod, dev_scenes, scene, pre
     kw = dict(seed=17, adaptive=True, mode="persistent", precision="fast", schedule=schedule)
     b, sb, stb = d.render(cam, spp, depth, samples_per_group=4, **kw)
     assert sb.min() >= min(16, spp) and sb.max() <= spp and ((sb < spp).any() or scene == "cornell")
-    runs = [("tiles", {}, {}), ("tiles_kcap4", dict(tile_kcap=4, tile_kinc=1, tile_margin=0.5), {}),
+    runs = [("tiles", {}, {}), ("tiles_one_launch", dict(tile_first_pass=1), {}),
+            ("tiles_two_launches", dict(tile_first_pass=2), {}),
+            ("tiles_kcap4", dict(tile_kcap=4, tile_kinc=1, tile_margin=0.5), {}),
+            ("tiles_one_launch_kcap3", dict(tile_kcap=3, tile_kinc=2, tile_first_pass=1), {}),
             ("tiles_kcap3", dict(tile_kcap=3, tile_kinc=2, tile_margin=2.0), {}),
             ("phases", {}, dict(adapt_phases=True)),
             ("phases_small", dict(phase_slots=1024, phase_kcap=8), dict(adapt_phases=True))]

@@ -158,6 +158,8 @@ def test_adaptive_recorded_segments_equal_oracle(rtx_mod, orc, scenes, acase, ro
 FULL_BUDGET_CASES = [(1, 200, 0.7), (3, 2048, 0.5)]  # bench case index, spp, band row (fraction of H)
 TUNES = {"tiles": ({}, False), "tiles_small": (dict(tile_kcap=8, tile_kinc=4, tile_margin=0.75), False),
          "tiles_one": (dict(tile_kcap=1, tile_kinc=1), False), "phases": ({}, True),
+         "tiles_one_launch": (dict(tile_first_pass=1), False),
+         "tiles_one_launch_small": (dict(tile_first_pass=1, tile_kcap=8, tile_kinc=4), False),
          "phases_small": (dict(phase_slots=4096, phase_kcap=8), True)}
 
 
