@@ -371,6 +371,7 @@ int build_fast4(const rtx_bvh_node* n, const rtx_prim* prims, std::vector<F4Node
 // the planes; every lower plane byte is the largest q with fmaf(q, s, o) <= the f32 plane and
 // every upper one the smallest q with fmaf(q, s, o) >= it, the device's own decode (one
 // rounding), so the decoded box contains the f32 box.  false: a non-finite plane.
+#if RTX_QNODE
 static bool quantise_f4(const std::vector<F4Node>& f4, std::vector<QNode>& out) {
   out.assign(f4.size(), QNode{});
   for (size_t i = 0; i < f4.size(); i++) {
@@ -419,6 +420,7 @@ static bool quantise_f4(const std::vector<F4Node>& f4, std::vector<QNode>& out) 
   }
   return true;
 }
+#endif
 
 // Fast-path tree of our own: binned SAH on all three axes (32 bins)
 // over the conservative primitive boxes (prim_box), split down to one primitive per leaf;
@@ -548,23 +550,32 @@ static int build_global_prims(const rtx_prim* prims, int64_t n, int32_t out[2]) 
   return k;
 }
 
-// Slots (pixel x sample radiance records) a render keeps in flight: `want`, limited to half of
-// the device memory that is free or already held by this scene's slot buffers, so several
-// scenes on one device, or a smaller GPU, get smaller groups instead of RTX_ERR_NOMEM.
-// The free-memory query is made once per scene (the first render that sizes its slots; it
-// costs ~0.5 ms, too much per frame): scenes created later see what the earlier ones took.
-int64_t slot_target(rtx_scene* sc, int64_t bytes_per_slot, int64_t want) {
+// The allowance of a scene's slot buffers (the radiance records of the samples in flight, the
+// wavefront's path queues, the adaptive workspaces): half of the device memory that is free or
+// already held by them, so several scenes on one device, or a smaller GPU, get smaller groups
+// instead of RTX_ERR_NOMEM.  ONE allowance for all of them: a render holds only its own kind's
+// buffers (render_device_impl releases the others when the kind changes) and sizes them
+// within the allowance minus what its other buffers take.  The free-memory query is made once
+// per scene (the first render that sizes its slots; it costs ~0.5 ms, too much per frame):
+// scenes created later see what the earlier ones took.
+double slot_allowance(rtx_scene* sc) {
   if (sc->slot_mem < 0) {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
       (void)hipGetLastError();
       fr = (size_t)1 << 62;
     }
-    double held = (double)sc->lbuf.n + (double)sc->queue[0].n + (double)sc->queue[1].n;
-    held += (double)sc->aw.lbuf.n + (double)sc->aw.smap.n;
+    double held = (double)sc->lbuf.n + (double)sc->queue[0].n + (double)sc->queue[1].n + (double)sc->segs1.n;
+    held += (double)sc->aw.lbuf.n + (double)sc->aw.smap.n + (double)sc->aw.segs.n;
     sc->slot_mem = 0.5 * ((double)fr + held);
   }
-  return std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)(sc->slot_mem / (double)bytes_per_slot)));
+  return sc->slot_mem;
+}
+// Slots a render keeps in flight: `want`, within the allowance less `other` bytes the render's
+// other slot buffers take.
+int64_t slot_target(rtx_scene* sc, int64_t bytes_per_slot, int64_t want, double other = 0.0) {
+  const double mem = std::max(0.0, slot_allowance(sc) - other);
+  return std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)(mem / (double)bytes_per_slot)));
 }
 
 int pick_stack(int depth) {
@@ -783,9 +794,15 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   // kTileNT tiles of kTileTP pixels x kcap slots (24 B of radiance each)
   const int64_t max_blocks = 4ll * sc->cus;
   const int64_t max_tiles = (npix + kTileTP - 1) / kTileTP;
+  const bool one_launch = tiles && (g_tune.tile_first_pass ? g_tune.tile_first_pass == 1 : kTileFirstPassInLaunch);
+  // the uniform first pass's radiance (and segment) records, in the scene's buffers
+  const double first_bytes = one_launch ? 0.0 : (double)npix * K1 * (3 * sizeof(double) + (L.count ? 2 : 0));
   int32_t kcap;
   if (tiles) {
     kcap = std::max(1, std::min(budget, g_tune.tile_kcap > 0 ? g_tune.tile_kcap : kTileKcap));
+    // within the allowance: a pixel's batches get smaller, not the launch
+    const int64_t per_k = max_blocks * kTileNT * kTileTP * (int64_t)(3 * sizeof(double) + (L.count ? 2 : 0));
+    kcap = (int32_t)std::min<int64_t>(kcap, slot_target(sc, per_k, kcap, first_bytes));
     const int64_t slots = max_blocks * kTileNT * kTileTP * (int64_t)kcap;
     if ((rc = w.lbuf.reserve(slots * 3 * sizeof(double)))) return rc;
     if (L.count && (rc = w.segs.reserve(slots * sizeof(uint16_t)))) return rc;
@@ -799,8 +816,9 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     if ((rc = w.targs.reserve(sizeof(TileArgs)))) return rc;
     if ((rc = w.ctr.reserve(8 * 16 * sizeof(unsigned long long) + 64))) return rc;
   } else {
-    // slots after the first phase: 24 B of radiance + 8 B of slot map each
-    const int64_t cap = std::min<int64_t>(0xFFFFFFFFll, slot_target(sc, 32, 1ll << kSlotTargetLog2));
+    // slots after the first phase: 24 B of radiance + 8 B of slot map each (+ 2 B of segments)
+    const int64_t cap =
+        std::min<int64_t>(0xFFFFFFFFll, slot_target(sc, 32 + (L.count ? 2 : 0), 1ll << kSlotTargetLog2, first_bytes));
     if (npix * 4 > cap) return fail(RTX_ERR_NOMEM, "adaptive render: too many pixels for the device memory");
     kcap = (int32_t)std::min<int64_t>(budget, std::max<int64_t>(4, (cap / npix) & ~3ll));
     if (g_tune.phase_kcap > 0) kcap = std::min(kcap, g_tune.phase_kcap);
@@ -891,7 +909,6 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   };
   // the first pass inside the tile launch: tiles of every pixel in image order, each starting
   // with min_spp samples per pixel (no uniform launch, no record kernel, no claim-order sort)
-  const bool one_launch = tiles && (g_tune.tile_first_pass ? g_tune.tile_first_pass == 1 : kTileFirstPassInLaunch);
   if (one_launch) {
     RenderArgs Ag = A;
     Ag.L = w.lbuf.as<double>(), Ag.conv = nullptr, Ag.K = 1, Ag.s0 = 0;
@@ -1361,6 +1378,19 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   // (render_adaptive); an explicit samples_per_group keeps uniform groups
   const bool phased = prm->mode == RTX_MODE_PERSISTENT && prm->adaptive && !mk_adaptive &&
                       prm->samples_per_group <= 0 && budget > 0 && npix > 0;
+  // a render keeps only its own kind of slot buffers (one allowance, slot_allowance): the
+  // adaptive workspaces go when a uniform-group render comes, the wavefront's queues when a
+  // persistent one does, and an adaptive render keeps of the scene's radiance buffer at most
+  // twice what its uniform first pass needs
+  if (phased) {
+    const size_t first = (size_t)npix * std::min(std::max(1, prm->min_spp), budget) * 3 * sizeof(double);
+    if (sc->lbuf.n > 2 * first) sc->lbuf.release();
+    for (auto& q : sc->queue) q.release();
+  } else {
+    sc->aw.lbuf.release(), sc->aw.smap.release(), sc->aw.segs.release(), sc->segs1.release();
+    if (prm->mode != RTX_MODE_WAVEFRONT)
+      for (auto& q : sc->queue) q.release();
+  }
 
   int rc;
   if ((rc = sc->px_sum.reserve(npix * 3 * sizeof(double)))) return rc;
