@@ -115,6 +115,9 @@ constexpr int kTileKcap = 128;
 constexpr int kTileKinc = 8;
 constexpr double kTileMargin = 1.0;
 constexpr bool kTileFirstPassInLaunch = false;  // the first pass inside the tile launch (else a uniform launch of its own)
+constexpr int kTileTPDefault = 32, kTileNTDefault = 8;  // pixels per tile, tiles in flight per workgroup
+constexpr double kTileMarginStep = 0.0;  // the margin's growth per batch of a tile
+constexpr int kTileTail = 0;             // pixels left in a tile that take the rest of their budget at once
 // Overrides of the adaptive schedules' constants (0: the default): rtx_internal_adapt_tune, a
 // test and tuning hook (not in rtx.h) that forces small workspaces and floors, so the paths
 // that only a large frame at a large budget reaches run on small frames too.
@@ -124,8 +127,11 @@ struct AdaptTune {
   int64_t phase_slots;  // phases: the smallest phase planned while pixels remain (kAdaptPhaseSlots)
   int phase_kcap;       // phases: the largest batch of one pixel (else from the workspace)
   int tile_first_pass;  // tiles: 1 the first pass in the tile launch too, 2 in a launch of its own (0: default)
+  int tile_tp, tile_nt;  // tiles: pixels per tile, tiles in flight per workgroup (0: default)
+  double tile_mstep;     // tiles: margin growth per batch (< 0: default)
+  int tile_tail;         // tiles: pixels left that take the rest of their budget (< 0: default)
 };
-static AdaptTune g_tune{};
+static AdaptTune g_tune{0, 0, 0.0, 0, 0, 0, 0, 0, -1.0, -1};
 struct AdaptWs {
   DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer, [134] TileArgs
   DevBuf segs;                                  // counting renders: each slot's path segments (u16)
@@ -793,7 +799,9 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   // tile schedule: room for every block the launch can hold (4 per CU at 128 VGPRs), each with
   // kTileNT tiles of kTileTP pixels x kcap slots (24 B of radiance each)
   const int64_t max_blocks = 4ll * sc->cus;
-  const int64_t max_tiles = (npix + kTileTP - 1) / kTileTP;
+  const int tp = std::max(1, std::min(kTileTP, g_tune.tile_tp > 0 ? g_tune.tile_tp : kTileTPDefault));
+  const int ntl = std::max(1, std::min(kTileNT, g_tune.tile_nt > 0 ? g_tune.tile_nt : kTileNTDefault));
+  const int64_t max_tiles = (npix + tp - 1) / tp;
   const bool one_launch = tiles && (g_tune.tile_first_pass ? g_tune.tile_first_pass == 1 : kTileFirstPassInLaunch);
   // the uniform first pass's radiance (and segment) records, in the scene's buffers
   const double first_bytes = one_launch ? 0.0 : (double)npix * K1 * (3 * sizeof(double) + (L.count ? 2 : 0));
@@ -801,9 +809,9 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   if (tiles) {
     kcap = std::max(1, std::min(budget, g_tune.tile_kcap > 0 ? g_tune.tile_kcap : kTileKcap));
     // within the allowance: a pixel's batches get smaller, not the launch
-    const int64_t per_k = max_blocks * kTileNT * kTileTP * (int64_t)(3 * sizeof(double) + (L.count ? 2 : 0));
+    const int64_t per_k = max_blocks * ntl * tp * (int64_t)(3 * sizeof(double) + (L.count ? 2 : 0));
     kcap = (int32_t)std::min<int64_t>(kcap, slot_target(sc, per_k, kcap, first_bytes));
-    const int64_t slots = max_blocks * kTileNT * kTileTP * (int64_t)kcap;
+    const int64_t slots = max_blocks * ntl * tp * (int64_t)kcap;
     if ((rc = w.lbuf.reserve(slots * 3 * sizeof(double)))) return rc;
     if (L.count && (rc = w.segs.reserve(slots * sizeof(uint16_t)))) return rc;
     for (DevBuf* b : {&w.k[0], &w.k[1], &w.off, &w.act})
@@ -835,6 +843,8 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   }
   const double tile_margin = g_tune.tile_margin > 0 ? g_tune.tile_margin : kTileMargin;
   const int32_t tile_kinc = g_tune.tile_kinc > 0 ? g_tune.tile_kinc : kTileKinc;
+  const double tile_mstep = g_tune.tile_mstep >= 0 ? g_tune.tile_mstep : kTileMarginStep;
+  const int32_t tile_tail = g_tune.tile_tail >= 0 ? g_tune.tile_tail : kTileTail;
   unsigned long long* ctr = w.ctr.as<unsigned long long>();  // 8 region counters, then the slot count, ...
   const unsigned qb = (unsigned)((npix + kBlock - 1) / kBlock);
   // record + next batch sizes after phase g (its slots in Lph: the uniform first phase's, or the
@@ -914,8 +924,8 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     Ag.L = w.lbuf.as<double>(), Ag.conv = nullptr, Ag.K = 1, Ag.s0 = 0;
     RegionCounts rcn{};
     const int64_t nt = max_tiles;
-    for (int r = 0; r < 8; r++) {  // tile t's region: min(7, kTileTP * t * 8 / npix)
-      auto first_tile = [&](int64_t q) { return std::min<int64_t>(nt, (q * npix + 8 * kTileTP - 1) / (8 * kTileTP)); };
+    for (int r = 0; r < 8; r++) {  // tile t's region: min(7, tp * t * 8 / npix)
+      auto first_tile = [&](int64_t q) { return std::min<int64_t>(nt, (q * npix + 8 * tp - 1) / (8 * tp)); };
       rcn.c[r] = (uint32_t)((r == 7 ? nt : first_tile(r + 1)) - first_tile(r));
     }
     TileArgs ta{};
@@ -927,7 +937,8 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ta.px = px, ta.npix = npix;
     ta.kcap = kcap, ta.min_spp = prm->min_spp, ta.budget = budget, ta.kinc = tile_kinc;
     ta.max_blocks = (int32_t)max_blocks, ta.k1 = std::min(K1, kcap);  // (a batch never exceeds kcap)
-    ta.rel = prm->rel_threshold, ta.margin = tile_margin;
+    ta.tp = tp, ta.nt = ntl, ta.tail_px = tile_tail;
+    ta.rel = prm->rel_threshold, ta.margin = tile_margin, ta.margin_step = tile_mstep;
     hipLaunchKernelGGL(k_tile_setup, dim3(1), dim3(1), 0, s, ta, w.targs.as<TileArgs>(), ctr, rcn, (uint32_t)npix,
                        w.tcount.as<uint32_t>());
     HIPC(hipGetLastError());
@@ -966,7 +977,8 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     HIPC(hipGetLastError());
     const unsigned tb = (unsigned)std::max<int64_t>(1, (max_tiles + kBlock - 1) / kBlock);
     hipLaunchKernelGGL(k_tile_keys, dim3(tb), dim3(kBlock), 0, s, (const uint32_t*)w.act.as<uint32_t>(),
-                       (const uint32_t*)(tc + 8), (const uint32_t*)knext, npix, max_tiles, w.tkeys[0].as<uint32_t>(),
+                       (const uint32_t*)(tc + 8), (const uint32_t*)knext, npix, max_tiles, (int32_t)tp,
+                       w.tkeys[0].as<uint32_t>(),
                        w.tvals[0].as<uint32_t>(), tc);
     HIPC(hipGetLastError());
     HIPC(rtxscan::sort_pairs_u32(w.tkeys[0].as<uint32_t>(), w.tkeys[1].as<uint32_t>(), w.tvals[0].as<uint32_t>(),
@@ -980,7 +992,8 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ta.px = px, ta.npix = npix;
     ta.kcap = kcap, ta.min_spp = prm->min_spp, ta.budget = budget, ta.kinc = tile_kinc;
     ta.max_blocks = (int32_t)max_blocks, ta.k1 = K1;
-    ta.rel = prm->rel_threshold, ta.margin = tile_margin;
+    ta.tp = tp, ta.nt = ntl, ta.tail_px = tile_tail;
+    ta.rel = prm->rel_threshold, ta.margin = tile_margin, ta.margin_step = tile_mstep;
     hipLaunchKernelGGL(k_tile_setup, dim3(1), dim3(1), 0, s, ta, w.targs.as<TileArgs>(), ctr, RegionCounts{},
                        (uint32_t)npix, w.tcount.as<uint32_t>());
     HIPC(hipGetLastError());
@@ -1564,8 +1577,8 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     HIPC(hipGetLastError());
   }
   if (timed) {  // the statistics come back with the frame: one wait on the end event, no blocking copy after it
-    if ((rc = sc->counters_h.reserve(10 * sizeof(unsigned long long)))) return rc;
-    HIPC(hipMemcpyAsync(sc->counters_h.p, cnt, 10 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    if ((rc = sc->counters_h.reserve(12 * sizeof(unsigned long long)))) return rc;
+    HIPC(hipMemcpyAsync(sc->counters_h.p, cnt, 12 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     HIPC(hipEventRecord(sc->ev[1], s));
   }
   if (banded) {  // the caller's stream owns the output again once the band copies are done
@@ -1583,8 +1596,10 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
       HIPC(hipEventElapsedTime(&hms, sc->evpool[e], sc->evpool[e + 1]));
       hot_ms += hms;
     }
-    unsigned long long h[10];
+    unsigned long long h[12];
     std::memcpy(h, sc->counters_h.p, sizeof h);
+    stats->wave_rounds = h[10];
+    stats->wave_rounds_idle = h[11];
     stats->rays_total = h[0];
     stats->parked = L.park ? 1 : 0;
     stats->rays_primary = h[1];
@@ -1754,6 +1769,7 @@ int rtx_render_multi(rtx_scene* const* scenes, int32_t n, const rtx_camera* cam,
       a.wave_node_iters += st[k].wave_node_iters, a.wave_prim_iters += st[k].wave_prim_iters;
       a.tri_tests += st[k].tri_tests, a.sphere_tests += st[k].sphere_tests;
       a.rays_recorded += st[k].rays_recorded;
+      a.wave_rounds += st[k].wave_rounds, a.wave_rounds_idle += st[k].wave_rounds_idle;
       a.node_bytes = st[k].node_bytes, a.parked |= st[k].parked, a.build |= st[k].build;
     }
     *stats = a;
@@ -1926,11 +1942,14 @@ extern "C" int rtx_internal_check_sincos(int device, int64_t n, uint64_t seed, i
 // largest batch.  Results never depend on them, only the amount of work and the number of
 // phases do (tests/test_gpu_timed.py runs the full budgets through forced small workspaces).
 extern "C" int rtx_internal_adapt_tune(int32_t tile_kcap, int32_t tile_kinc, double tile_margin, int64_t phase_slots,
-                                       int32_t phase_kcap, int32_t tile_first_pass) {
+                                       int32_t phase_kcap, int32_t tile_first_pass, int32_t tile_tp, int32_t tile_nt,
+                                       double tile_mstep, int32_t tile_tail) {
   if (tile_kcap < 0 || tile_kinc < 0 || !(tile_margin >= 0) || phase_slots < 0 || phase_kcap < 0 ||
-      tile_first_pass < 0 || tile_first_pass > 2)
+      tile_first_pass < 0 || tile_first_pass > 2 || tile_tp < 0 || tile_tp > kTileTP || tile_nt < 0 ||
+      tile_nt > kTileNT)
     return fail(RTX_ERR_INVALID, "bad tuning value");
-  g_tune = AdaptTune{tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap, tile_first_pass};
+  g_tune = AdaptTune{tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap, tile_first_pass, tile_tp, tile_nt,
+                     tile_mstep, tile_tail};
   return RTX_OK;
 }
 

@@ -613,6 +613,7 @@ struct Counters {
   uint32_t nodes, prims;  // lane-level node visits / primitive tests
   uint32_t wnodes, wprims;  // wave-level loop iterations (counted by the first active lane)
   uint32_t tris, sphs;      // primitive tests by kind (rects = prims - tris - sphs)
+  uint32_t witers, widle;   // persistent kernel: wave loop rounds, and those with no path to trace
 };
 __device__ __forceinline__ void count_prim(Counters& c, const rtx_prim* P) {
   c.prims++;

@@ -140,8 +140,8 @@ struct PersistLds {
 // release / acquire), so no cross-XCD visibility is needed.  Largest tiles first keeps the
 // launch's end short: the last tiles claimed are the cheapest.
 // ---------------------------------------------------------------------------------------
-constexpr int kTileTP = 32;  // pixels per tile (the record runs one lane per pixel)
-constexpr int kTileNT = 8;   // tiles in flight per workgroup
+constexpr int kTileTP = 32;  // most pixels per tile (the record runs one lane per pixel; TileArgs::tp)
+constexpr int kTileNT = 16;  // most tiles in flight per workgroup (TileArgs::nt)
 struct PixelSoA {
   double *sum, *mean, *m2;  // 3 x npix each (channel-major)
   int32_t* samples;
@@ -151,11 +151,11 @@ struct PixelSoA {
 // counter block, like the slot map's in MAP == 1 launches).
 struct TileArgs {
   const uint32_t* act;     // subset pixels still sampling after the first pass, in image order
-  const uint32_t* order;   // tile ids (tile t = act[t * kTileTP ...]) in claim order, region by region
+  const uint32_t* order;   // tile ids (tile t = act[t * tp ...]) in claim order, region by region
   const uint32_t* rcount;  // tiles of each of the 8 regions
   const uint32_t* knext;   // each pixel's first batch (k_adapt_record of the first pass)
   const uint32_t* nact;    // the number of active pixels
-  double* L;               // radiance: kTileTP * kcap slots per (block, descriptor)
+  double* L;               // radiance: tp * kcap slots per (block, descriptor)
   uint16_t* segs;          // counting builds: each slot's path segments (same indexing), else null
   unsigned long long* rec_segs;  // counting builds: segments of the recorded samples
   PixelSoA px;
@@ -166,7 +166,12 @@ struct TileArgs {
   int32_t max_blocks;  // blocks the radiance workspace has room for
   int32_t k1;          // act == nullptr: the launch runs the first pass too (every pixel, tiles in
                        // image order, first batch k1 = min_spp samples; order and knext unused)
+  int32_t tp, nt;      // pixels per tile (<= kTileTP), tiles in flight per workgroup (<= kTileNT)
+  int32_t tail_px;     // a tile with at most this many pixels left sampling gives them the rest of
+                       // their budget (within kcap) in one batch: no further phase chains
+  int32_t pad_;
   double rel, margin;
+  double margin_step;  // the margin grows by this much with every batch of the tile
 };
 // A tile in flight (LDS).  word = (cursor << 32) | T: the batch's T slots are claimed by
 // adding to the cursor (an add returns the phase's T with it, so a claim is consistent even
@@ -175,7 +180,7 @@ struct TileArgs {
 // off[i + 1].  state: 0 free, 1 being initialised, 2 in flight.
 struct TileDesc {
   unsigned long long word;
-  uint32_t rem, state, npx, pad_;
+  uint32_t rem, state, npx, phase;
   uint32_t off[kTileTP + 1];
   uint32_t pix[kTileTP];
   uint32_t s0[kTileTP];
@@ -226,6 +231,8 @@ __device__ __forceinline__ void flush_counters(const RenderArgs& A, const Counte
     atomicAdd(&A.counters[5], (unsigned long long)c.wprims);
     atomicAdd(&A.counters[6], (unsigned long long)c.tris);
     atomicAdd(&A.counters[7], (unsigned long long)c.sphs);
+    if (c.witers) atomicAdd(&A.counters[10], (unsigned long long)c.witers);
+    if (c.widle) atomicAdd(&A.counters[11], (unsigned long long)c.widle);
   }
   if (segs) atomicAdd(&A.counters[0], (unsigned long long)segs);
   if (prims) atomicAdd(&A.counters[1], (unsigned long long)prims);
@@ -454,7 +461,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 // channel, so the batch is that many more samples (times the margin), at least kinc, within
 // the budget and the workspace.  Only the amount of work depends on it, never the result: a
 // sample traced past the pixel's convergence point is discarded by the record.
-__device__ __forceinline__ uint32_t tile_next_batch(const PixRec& r, const TileArgs* ta) {
+__device__ __forceinline__ uint32_t tile_next_batch(const PixRec& r, const TileArgs* ta, uint32_t phase) {
   const double rel = ta->rel;
   double need = 0.0;
   for (int c = 0; c < 3; c++) {
@@ -463,22 +470,23 @@ __device__ __forceinline__ uint32_t tile_next_batch(const PixRec& r, const TileA
     need = fmax(need, var / (rel * rel * mu * mu));
   }
   const int left = ta->budget - r.n;
-  const double want = (need - (double)r.n) * ta->margin;
+  const double want = (need - (double)r.n) * (ta->margin + ta->margin_step * (double)phase);
   int k = (want < (double)left) ? (int)ceil(want) : left;  // NaN / inf: the whole budget
   k = max(k, min(ta->kinc, left));
   return (uint32_t)min(k, min(left, ta->kcap));
 }
 // Slot index of the tile workspace: descriptor j of this block, batch slot s.
 __device__ __forceinline__ uint64_t tile_slot(const TileArgs* ta, int j, uint32_t s) {
-  return ((uint64_t)(blockIdx.x * (uint32_t)kTileNT + (uint32_t)j) * kTileTP) * (uint64_t)ta->kcap + s;
+  return ((uint64_t)(blockIdx.x * (uint32_t)ta->nt + (uint32_t)j) * (uint32_t)ta->tp) * (uint64_t)ta->kcap + s;
 }
 // Claims a free descriptor and the next tile in claim order (this block's region first, then
 // the others) and lays out the tile's first batch (wave-uniform; the whole wave).  false: no
 // free descriptor, or the claim order is used up (then tl->exhausted is set).
 __device__ __forceinline__ bool tile_claim(TileLds* tl, const TileArgs* ta, unsigned long long* ctr, uint32_t region) {
   int j = -1;
+  const int nt = ta->nt;
   if (lane_id() == 0)
-    for (int q = 0; q < kTileNT; q++)
+    for (int q = 0; q < nt; q++)
       if (atomicCAS(&tl->d[q].state, 0u, 1u) == 0u) {
         j = q;
         break;
@@ -506,8 +514,8 @@ __device__ __forceinline__ bool tile_claim(TileLds* tl, const TileArgs* ta, unsi
     }
     return false;
   }
-  const uint32_t first = (uint32_t)tid * kTileTP, nact = *ta->nact;
-  const int n = (int)min<uint32_t>(kTileTP, nact - first);
+  const uint32_t first = (uint32_t)tid * (uint32_t)ta->tp, nact = *ta->nact;
+  const int n = (int)min<uint32_t>((uint32_t)ta->tp, nact - first);
   const int i = (int)lane_id();
   uint32_t p = 0, k = 0, s = 0;
   if (i < n) {
@@ -518,7 +526,7 @@ __device__ __forceinline__ bool tile_claim(TileLds* tl, const TileArgs* ta, unsi
   const uint32_t inc = wave_incl_scan(k);
   const uint32_t T = __shfl(inc, 63);
   if (i < n) d.pix[i] = p, d.s0[i] = s, d.off[i] = inc - k;
-  if (i == 0) d.off[n] = T, d.npx = (uint32_t)n, d.rem = T;
+  if (i == 0) d.off[n] = T, d.npx = (uint32_t)n, d.rem = T, d.phase = 0;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the layout before the claim word
   if (i == 0) {
     atomicExch(&d.word, (unsigned long long)T);
@@ -549,14 +557,17 @@ __device__ __forceinline__ void tile_record(TileLds* tl, const TileArgs* ta, int
         atomicAdd(ta->rec_segs, t);
       }
       store_pixel(r, ta->px, ta->npix, p);
-      if (!r.conv && r.n < ta->budget) kn = tile_next_batch(r, ta);
+      if (!r.conv && r.n < ta->budget) kn = tile_next_batch(r, ta, d.phase);
     }
     nrec = (uint32_t)r.n;
   }
+  // few pixels left sampling: the rest of their budget now, rather than more phases of a few paths
+  if ((int)__popcll(__ballot(kn != 0)) <= ta->tail_px && kn != 0)
+    kn = (uint32_t)min(ta->budget - (int)nrec, ta->kcap);
   const uint32_t inc = wave_incl_scan(kn);
   const uint32_t T = __shfl(inc, 63);
   if (i < n) d.off[i] = inc - kn, d.s0[i] = nrec;
-  if (i == 0) d.off[n] = T, d.rem = T;
+  if (i == 0) d.off[n] = T, d.rem = T, d.phase = d.phase + 1;
   // the statistics (global) and the layout (LDS) complete before the next batch is claimable
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   if (i == 0) {
@@ -668,7 +679,8 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
         const uint32_t nidle = (uint32_t)__popcll(idle);
         const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane_id()) - 1ull));
         uint32_t given = 0;
-        for (int j = 0; j < kTileNT && given < nidle; j++) {
+        const int nt = ta->nt;
+        for (int j = 0; j < nt && given < nidle; j++) {
           const unsigned long long w = *(volatile unsigned long long*)&tl->d[j].word;
           const uint32_t wc = __builtin_amdgcn_readfirstlane((uint32_t)(w >> 32));
           const uint32_t wt = __builtin_amdgcn_readfirstlane((uint32_t)w);
@@ -769,7 +781,9 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
         if (COUNT) pseg = 0;
       }
     }
+    if (COUNT && lane_id() == 0) c.witers++;  // (the loop's rounds are wave-uniform: lane 0 counts)
     if (!__any(has)) {
+      if (COUNT && lane_id() == 0) c.widle++;
       if (kTiles) {  // nothing to trace now: leave once no tile is left or in flight, else wait
         if (__builtin_amdgcn_readfirstlane(tiles_done(tl) ? 1u : 0u)) break;
         __builtin_amdgcn_s_sleep(2);
@@ -1117,18 +1131,18 @@ __global__ __launch_bounds__(kBlock) void k_tile_compact(const uint32_t* __restr
 __global__ __launch_bounds__(kBlock) void k_tile_keys(const uint32_t* __restrict__ act,
                                                       const uint32_t* __restrict__ nact,
                                                       const uint32_t* __restrict__ knext, int64_t npix,
-                                                      int64_t max_tiles, uint32_t* __restrict__ keys,
+                                                      int64_t max_tiles, int32_t tp, uint32_t* __restrict__ keys,
                                                       uint32_t* __restrict__ vals, uint32_t* __restrict__ rcount) {
   const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (t >= max_tiles) return;
-  const int64_t first = t * kTileTP, na = *nact;
+  const int64_t first = t * tp, na = *nact;
   vals[t] = (uint32_t)t;
   if (first >= na) {
     keys[t] = 0xFFFFFFFFu;  // no such tile: sorted after every region
     return;
   }
   uint32_t work = 0;
-  for (int64_t i = first; i < min<int64_t>(first + kTileTP, na); i++) work += knext[act[i]];
+  for (int64_t i = first; i < min<int64_t>(first + tp, na); i++) work += knext[act[i]];
   const uint32_t region = (uint32_t)min<int64_t>(7, ((int64_t)act[first] * 8) / max<int64_t>(1, npix));
   keys[t] = (region << 24) | (0xFFFFFFu - min(work, 0xFFFFFFu));
   atomicAdd(&rcount[region], 1u);

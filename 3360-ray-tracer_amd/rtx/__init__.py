@@ -106,7 +106,8 @@ class Stats(C.Structure):
                 ("node_visits", C.c_uint64), ("prim_tests", C.c_uint64),
                 ("node_bytes", C.c_uint64), ("wave_node_iters", C.c_uint64), ("wave_prim_iters", C.c_uint64),
                 ("tri_tests", C.c_uint64), ("sphere_tests", C.c_uint64), ("parked", C.c_uint64),
-                ("build", C.c_uint64), ("rays_recorded", C.c_uint64)]
+                ("build", C.c_uint64), ("rays_recorded", C.c_uint64), ("wave_rounds", C.c_uint64),
+                ("wave_rounds_idle", C.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -350,16 +351,18 @@ class DeviceScene:
         return st.as_dict() if stats else None
 
 
-def adapt_tune(tile_kcap=0, tile_kinc=0, tile_margin=0.0, phase_slots=0, phase_kcap=0, tile_first_pass=0):
+def adapt_tune(tile_kcap=0, tile_kinc=0, tile_margin=0.0, phase_slots=0, phase_kcap=0, tile_first_pass=0,
+               tile_tp=0, tile_nt=0, tile_mstep=-1.0, tile_tail=-1):
     """Test / tuning hook (rtx_internal_adapt_tune, not in rtx.h): overrides of the adaptive
     schedules' constants for the renders that follow in this process; no argument (all 0)
     restores the defaults.  Results never depend on them, only the work and the phases do.
     tile_first_pass: 1 the first pass inside the tile launch, 2 a uniform launch of its own."""
     f = lib().rtx_internal_adapt_tune
-    f.argtypes = [C.c_int32, C.c_int32, C.c_double, C.c_int64, C.c_int32, C.c_int32]
+    f.argtypes = [C.c_int32, C.c_int32, C.c_double, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
+                  C.c_double, C.c_int32]
     f.restype = C.c_int
-    _check(f(tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap, tile_first_pass),
-           "rtx_internal_adapt_tune")
+    _check(f(tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap, tile_first_pass, tile_tp, tile_nt,
+             tile_mstep, tile_tail), "rtx_internal_adapt_tune")
 
 
 def render_multi(scenes, cam, spp, max_depth, seed=1234, adaptive=True, mode="persistent", precision="fast",

@@ -168,7 +168,7 @@ def main():
 
     if args.adapt_tune:
         kv = dict(x.split("=") for x in args.adapt_tune.split(","))
-        rtx.adapt_tune(**{k: (float(v) if k == "tile_margin" else int(v)) for k, v in kv.items()})
+        rtx.adapt_tune(**{k: (float(v) if k in ("tile_margin", "tile_mstep") else int(v)) for k, v in kv.items()})
     workload = args.workload if args.workload != "auto" else ("c3_bunny" if world == 1 else "c4_bunny4k")
     scene_name, preset, width, spp, depth = WORKLOADS[workload]
     spp = args.spp or spp
@@ -283,6 +283,7 @@ def main():
                                   "served from L2/MALL (the scene is cache-resident), not an HBM figure"},
         "nodes_per_segment": nodes_per_seg, "prims_per_segment": prims_per_seg, "boxes_per_visit": boxes_per_visit,
         "simd_efficiency_nodes": simd_nodes, "simd_efficiency_prims": simd_prims,
+        "wave_rounds_idle_frac": cst["wave_rounds_idle"] / cst["wave_rounds"] if cst["wave_rounds"] else None,
     })
 
     generic_leg = None
@@ -383,6 +384,7 @@ def time_adaptive(torch, step, params, per_frame_fixed, fixed_value):
     el = time.perf_counter() - t0
     cst = step(params(ap.flags | 1, adaptive=True))  # RTX_FLAG_COUNT
     rec, traced = cst["rays_recorded"], sum(s["rays_total"] for s in sts) / n
+    idle = cst["wave_rounds_idle"] / cst["wave_rounds"] if cst["wave_rounds"] else None
     hot_ms = sum(s["hot_kernel_ms"] for s in sts) / n
     return {"metric": "Mrays/s of the recorded samples' segments, adaptive sampling (the reference's default)",
             "value": rec * n / el / 1e6, "traced_value": traced * n / el / 1e6, "unit": "Mrays/s",
@@ -390,7 +392,7 @@ def time_adaptive(torch, step, params, per_frame_fixed, fixed_value):
             "hot_launches_per_step": sts[-1]["hot_launches"],
             "rays_recorded_per_step": rec, "rays_traced_per_step": traced,
             "recorded_fraction_of_traced": rec / max(1.0, traced), "vs_fixed_spp_value": rec * n / el / 1e6 / fixed_value,
-            "schedule": "phases" if ap.flags & 32 else "tiles",
+            "schedule": "phases" if ap.flags & 32 else "tiles", "wave_rounds_idle_frac": idle,
             "sampling": sampling_text(True), "_recorded_whole": rec}
 
 

@@ -44,7 +44,8 @@ extern "C" {
 #define RTX_ABI_VERSION 7  /* 2: rtx_stats.node_bytes; 3: rtx_stats.parked, RTX_FLAG_PARK / NO_PARK;
                               4: rtx_stats.build, RTX_FLAG_GENERIC, rtx_render_multi;
                               5: RTX_FLAG_LEAF_STEP, RTX_BUILD_SPECULATIVE; 6: rtx_stats.rays_recorded;
-                              7: RTX_FLAG_ADAPT_PHASES (the adaptive tile schedule is the default) */
+                              7: RTX_FLAG_ADAPT_PHASES (the adaptive tile schedule is the default),
+                              rtx_stats.wave_rounds / wave_rounds_idle */
 
 enum {
   RTX_OK = 0,
@@ -253,6 +254,9 @@ typedef struct {
                                pixel's convergence and discard them: counted per sample.  Other adaptive
                                renders (wavefront, megakernel, explicit samples_per_group): 0 (not
                                counted).  0 without RTX_FLAG_COUNT */
+  uint64_t wave_rounds;      /* with RTX_FLAG_COUNT, persistent mode: rounds of the waves' loop (refill,
+                                segment), and those in which a wave had no path to trace (waiting for work) */
+  uint64_t wave_rounds_idle;
 } rtx_stats;
 
 /* ---- entry points ------------------------------------------------------------------ */
