@@ -1577,8 +1577,8 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     HIPC(hipGetLastError());
   }
   if (timed) {  // the statistics come back with the frame: one wait on the end event, no blocking copy after it
-    if ((rc = sc->counters_h.reserve(12 * sizeof(unsigned long long)))) return rc;
-    HIPC(hipMemcpyAsync(sc->counters_h.p, cnt, 12 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    if ((rc = sc->counters_h.reserve(13 * sizeof(unsigned long long)))) return rc;
+    HIPC(hipMemcpyAsync(sc->counters_h.p, cnt, 13 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     HIPC(hipEventRecord(sc->ev[1], s));
   }
   if (banded) {  // the caller's stream owns the output again once the band copies are done
@@ -1596,10 +1596,11 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
       HIPC(hipEventElapsedTime(&hms, sc->evpool[e], sc->evpool[e + 1]));
       hot_ms += hms;
     }
-    unsigned long long h[12];
+    unsigned long long h[13];
     std::memcpy(h, sc->counters_h.p, sizeof h);
     stats->wave_rounds = h[10];
     stats->wave_rounds_idle = h[11];
+    stats->wave_lanes_live = h[12];
     stats->rays_total = h[0];
     stats->parked = L.park ? 1 : 0;
     stats->rays_primary = h[1];
@@ -1770,6 +1771,7 @@ int rtx_render_multi(rtx_scene* const* scenes, int32_t n, const rtx_camera* cam,
       a.tri_tests += st[k].tri_tests, a.sphere_tests += st[k].sphere_tests;
       a.rays_recorded += st[k].rays_recorded;
       a.wave_rounds += st[k].wave_rounds, a.wave_rounds_idle += st[k].wave_rounds_idle;
+      a.wave_lanes_live += st[k].wave_lanes_live;
       a.node_bytes = st[k].node_bytes, a.parked |= st[k].parked, a.build |= st[k].build;
     }
     *stats = a;

@@ -614,6 +614,7 @@ struct Counters {
   uint32_t wnodes, wprims;  // wave-level loop iterations (counted by the first active lane)
   uint32_t tris, sphs;      // primitive tests by kind (rects = prims - tris - sphs)
   uint32_t witers, widle;   // persistent kernel: wave loop rounds, and those with no path to trace
+  uint32_t wlive;           // ... and the lanes with a path, summed over the rounds that trace
 };
 __device__ __forceinline__ void count_prim(Counters& c, const rtx_prim* P) {
   c.prims++;

@@ -233,6 +233,7 @@ __device__ __forceinline__ void flush_counters(const RenderArgs& A, const Counte
     atomicAdd(&A.counters[7], (unsigned long long)c.sphs);
     if (c.witers) atomicAdd(&A.counters[10], (unsigned long long)c.witers);
     if (c.widle) atomicAdd(&A.counters[11], (unsigned long long)c.widle);
+    if (c.wlive) atomicAdd(&A.counters[12], (unsigned long long)c.wlive);
   }
   if (segs) atomicAdd(&A.counters[0], (unsigned long long)segs);
   if (prims) atomicAdd(&A.counters[1], (unsigned long long)prims);
@@ -791,6 +792,10 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
       }
       if (exhausted) break;
       continue;
+    }
+    if (COUNT) {
+      const uint32_t live = (uint32_t)__popcll(__ballot(has));
+      if (lane_id() == 0) c.wlive += live;
     }
     if (!has) continue;
     // ---- one segment: closest hit + shading ----

@@ -107,7 +107,7 @@ class Stats(C.Structure):
                 ("node_bytes", C.c_uint64), ("wave_node_iters", C.c_uint64), ("wave_prim_iters", C.c_uint64),
                 ("tri_tests", C.c_uint64), ("sphere_tests", C.c_uint64), ("parked", C.c_uint64),
                 ("build", C.c_uint64), ("rays_recorded", C.c_uint64), ("wave_rounds", C.c_uint64),
-                ("wave_rounds_idle", C.c_uint64)]
+                ("wave_rounds_idle", C.c_uint64), ("wave_lanes_live", C.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

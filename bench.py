@@ -284,6 +284,8 @@ def main():
         "nodes_per_segment": nodes_per_seg, "prims_per_segment": prims_per_seg, "boxes_per_visit": boxes_per_visit,
         "simd_efficiency_nodes": simd_nodes, "simd_efficiency_prims": simd_prims,
         "wave_rounds_idle_frac": cst["wave_rounds_idle"] / cst["wave_rounds"] if cst["wave_rounds"] else None,
+        "lane_occupancy": (cst["wave_lanes_live"] / (64.0 * (cst["wave_rounds"] - cst["wave_rounds_idle"]))
+                           if cst["wave_rounds"] > cst["wave_rounds_idle"] else None),
     })
 
     generic_leg = None

@@ -257,6 +257,8 @@ typedef struct {
   uint64_t wave_rounds;      /* with RTX_FLAG_COUNT, persistent mode: rounds of the waves' loop (refill,
                                 segment), and those in which a wave had no path to trace (waiting for work) */
   uint64_t wave_rounds_idle;
+  uint64_t wave_lanes_live;  /* with RTX_FLAG_COUNT, persistent mode: lanes holding a path, summed over the
+                                rounds that trace (/ (64 x tracing rounds) = the rounds' lane occupancy) */
 } rtx_stats;
 
 /* ---- entry points ------------------------------------------------------------------ */
