@@ -118,6 +118,7 @@ constexpr bool kTileFirstPassInLaunch = false;  // the first pass inside the til
 constexpr int kTileTPDefault = 32, kTileNTDefault = 8;  // pixels per tile, tiles in flight per workgroup
 constexpr double kTileMarginStep = 0.0;  // the margin's growth per batch of a tile
 constexpr int kTileTail = 0;             // pixels left in a tile that take the rest of their budget at once
+constexpr double kTileStarveGain = 0.0;  // margin growth per idle wave of the block at a record
 // Overrides of the adaptive schedules' constants (0: the default): rtx_internal_adapt_tune, a
 // test and tuning hook (not in rtx.h) that forces small workspaces and floors, so the paths
 // that only a large frame at a large budget reaches run on small frames too.
@@ -130,8 +131,9 @@ struct AdaptTune {
   int tile_tp, tile_nt;  // tiles: pixels per tile, tiles in flight per workgroup (0: default)
   double tile_mstep;     // tiles: margin growth per batch (< 0: default)
   int tile_tail;         // tiles: pixels left that take the rest of their budget (< 0: default)
+  double tile_starve;    // tiles: margin growth per idle wave of the block at a record (< 0: default)
 };
-static AdaptTune g_tune{0, 0, 0.0, 0, 0, 0, 0, 0, -1.0, -1};
+static AdaptTune g_tune{0, 0, 0.0, 0, 0, 0, 0, 0, -1.0, -1, -1.0};
 struct AdaptWs {
   DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer, [134] TileArgs
   DevBuf segs;                                  // counting renders: each slot's path segments (u16)
@@ -845,6 +847,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   const int32_t tile_kinc = g_tune.tile_kinc > 0 ? g_tune.tile_kinc : kTileKinc;
   const double tile_mstep = g_tune.tile_mstep >= 0 ? g_tune.tile_mstep : kTileMarginStep;
   const int32_t tile_tail = g_tune.tile_tail >= 0 ? g_tune.tile_tail : kTileTail;
+  const double tile_starve = g_tune.tile_starve >= 0 ? g_tune.tile_starve : kTileStarveGain;
   unsigned long long* ctr = w.ctr.as<unsigned long long>();  // 8 region counters, then the slot count, ...
   const unsigned qb = (unsigned)((npix + kBlock - 1) / kBlock);
   // record + next batch sizes after phase g (its slots in Lph: the uniform first phase's, or the
@@ -938,7 +941,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ta.kcap = kcap, ta.min_spp = prm->min_spp, ta.budget = budget, ta.kinc = tile_kinc;
     ta.max_blocks = (int32_t)max_blocks, ta.k1 = std::min(K1, kcap);  // (a batch never exceeds kcap)
     ta.tp = tp, ta.nt = ntl, ta.tail_px = tile_tail;
-    ta.rel = prm->rel_threshold, ta.margin = tile_margin, ta.margin_step = tile_mstep;
+    ta.rel = prm->rel_threshold, ta.margin = tile_margin, ta.margin_step = tile_mstep, ta.starve_gain = tile_starve;
     hipLaunchKernelGGL(k_tile_setup, dim3(1), dim3(1), 0, s, ta, w.targs.as<TileArgs>(), ctr, rcn, (uint32_t)npix,
                        w.tcount.as<uint32_t>());
     HIPC(hipGetLastError());
@@ -993,7 +996,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ta.kcap = kcap, ta.min_spp = prm->min_spp, ta.budget = budget, ta.kinc = tile_kinc;
     ta.max_blocks = (int32_t)max_blocks, ta.k1 = K1;
     ta.tp = tp, ta.nt = ntl, ta.tail_px = tile_tail;
-    ta.rel = prm->rel_threshold, ta.margin = tile_margin, ta.margin_step = tile_mstep;
+    ta.rel = prm->rel_threshold, ta.margin = tile_margin, ta.margin_step = tile_mstep, ta.starve_gain = tile_starve;
     hipLaunchKernelGGL(k_tile_setup, dim3(1), dim3(1), 0, s, ta, w.targs.as<TileArgs>(), ctr, RegionCounts{},
                        (uint32_t)npix, w.tcount.as<uint32_t>());
     HIPC(hipGetLastError());
@@ -1945,13 +1948,13 @@ extern "C" int rtx_internal_check_sincos(int device, int64_t n, uint64_t seed, i
 // phases do (tests/test_gpu_timed.py runs the full budgets through forced small workspaces).
 extern "C" int rtx_internal_adapt_tune(int32_t tile_kcap, int32_t tile_kinc, double tile_margin, int64_t phase_slots,
                                        int32_t phase_kcap, int32_t tile_first_pass, int32_t tile_tp, int32_t tile_nt,
-                                       double tile_mstep, int32_t tile_tail) {
+                                       double tile_mstep, int32_t tile_tail, double tile_starve) {
   if (tile_kcap < 0 || tile_kinc < 0 || !(tile_margin >= 0) || phase_slots < 0 || phase_kcap < 0 ||
       tile_first_pass < 0 || tile_first_pass > 2 || tile_tp < 0 || tile_tp > kTileTP || tile_nt < 0 ||
       tile_nt > kTileNT)
     return fail(RTX_ERR_INVALID, "bad tuning value");
   g_tune = AdaptTune{tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap, tile_first_pass, tile_tp, tile_nt,
-                     tile_mstep, tile_tail};
+                     tile_mstep, tile_tail, tile_starve};
   return RTX_OK;
 }
 

@@ -172,6 +172,7 @@ struct TileArgs {
   int32_t pad_;
   double rel, margin;
   double margin_step;  // the margin grows by this much with every batch of the tile
+  double starve_gain;  // ... and by this much per wave of the block idle at the record (no work to claim)
 };
 // A tile in flight (LDS).  word = (cursor << 32) | T: the batch's T slots are claimed by
 // adding to the cursor (an add returns the phase's T with it, so a claim is consistent even
@@ -189,7 +190,8 @@ struct TileDesc {
 struct TileLds {
   uint32_t ready;      // descriptors whose batch has ended (to be recorded)
   uint32_t exhausted;  // the claim order is used up
-  uint32_t pad_[2];
+  uint32_t idle;       // waves of the block waiting for work (no path, nothing to claim)
+  uint32_t pad_;
   TileDesc d[kTileNT];
 };
 static_assert(sizeof(TileDesc) % 8 == 0 && sizeof(TileLds) % 8 == 0, "8-byte aligned tile descriptors");
@@ -462,7 +464,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 // channel, so the batch is that many more samples (times the margin), at least kinc, within
 // the budget and the workspace.  Only the amount of work depends on it, never the result: a
 // sample traced past the pixel's convergence point is discarded by the record.
-__device__ __forceinline__ uint32_t tile_next_batch(const PixRec& r, const TileArgs* ta, uint32_t phase) {
+__device__ __forceinline__ uint32_t tile_next_batch(const PixRec& r, const TileArgs* ta, uint32_t phase, uint32_t idle) {
   const double rel = ta->rel;
   double need = 0.0;
   for (int c = 0; c < 3; c++) {
@@ -471,7 +473,7 @@ __device__ __forceinline__ uint32_t tile_next_batch(const PixRec& r, const TileA
     need = fmax(need, var / (rel * rel * mu * mu));
   }
   const int left = ta->budget - r.n;
-  const double want = (need - (double)r.n) * (ta->margin + ta->margin_step * (double)phase);
+  const double want = (need - (double)r.n) * (ta->margin + ta->margin_step * (double)phase + ta->starve_gain * (double)idle);
   int k = (want < (double)left) ? (int)ceil(want) : left;  // NaN / inf: the whole budget
   k = max(k, min(ta->kinc, left));
   return (uint32_t)min(k, min(left, ta->kcap));
@@ -543,6 +545,7 @@ __device__ __forceinline__ void tile_record(TileLds* tl, const TileArgs* ta, int
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // every lane's radiance store, before its count-off
   const int i = (int)lane_id();
   const int n = (int)d.npx;
+  const uint32_t idle = *(volatile uint32_t*)&tl->idle;
   uint32_t kn = 0, nrec = 0;
   if (i < n) {
     const uint32_t p = d.pix[i], o0 = d.off[i], K = d.off[i + 1] - o0;
@@ -558,7 +561,7 @@ __device__ __forceinline__ void tile_record(TileLds* tl, const TileArgs* ta, int
         atomicAdd(ta->rec_segs, t);
       }
       store_pixel(r, ta->px, ta->npix, p);
-      if (!r.conv && r.n < ta->budget) kn = tile_next_batch(r, ta, d.phase);
+      if (!r.conv && r.n < ta->budget) kn = tile_next_batch(r, ta, d.phase, idle);
     }
     nrec = (uint32_t)r.n;
   }
@@ -655,6 +658,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   constexpr bool kPark = PARK > 0 && FAST && !SCATTER;
   const bool park_ok = kPark && A.S.use_bvh && !A.S.froot_leaf;
   bool parked = false;
+  bool waiting = false;  // (tile schedule: the wave is counted in tl->idle)
   TravState trs;
   while (true) {
     if constexpr (kTiles) {  // a tile whose batch has ended is recorded first (at most one per round)
@@ -787,11 +791,17 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
       if (COUNT && lane_id() == 0) c.widle++;
       if (kTiles) {  // nothing to trace now: leave once no tile is left or in flight, else wait
         if (__builtin_amdgcn_readfirstlane(tiles_done(tl) ? 1u : 0u)) break;
+        if (!waiting && lane_id() == 0) atomicAdd(&tl->idle, 1u);  // (records meanwhile size batches larger)
+        waiting = true;
         __builtin_amdgcn_s_sleep(2);
         continue;
       }
       if (exhausted) break;
       continue;
+    }
+    if (kTiles && waiting) {  // work again
+      if (lane_id() == 0) atomicSub(&tl->idle, 1u);
+      waiting = false;
     }
     if (COUNT) {
       const uint32_t live = (uint32_t)__popcll(__ballot(has));
