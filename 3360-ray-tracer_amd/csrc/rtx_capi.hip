@@ -115,7 +115,8 @@ constexpr int kTileKcap = 128;
 constexpr int kTileKinc = 8;
 constexpr double kTileMargin = 1.0;
 constexpr bool kTileFirstPassInLaunch = false;  // the first pass inside the tile launch (else a uniform launch of its own)
-constexpr int kTileTPDefault = 32, kTileNTDefault = 8;  // pixels per tile, tiles in flight per workgroup
+constexpr int kTileTPDefault = 8, kTileNTDefault = 8;  // pixels per tile, tiles in flight per workgroup
+constexpr int kTileSplit = 8;  // a pixel's predicted samples above this go in two pipelined batches
 constexpr double kTileMarginStep = 0.0;  // the margin's growth per batch of a tile
 constexpr int kTileTail = 0;             // pixels left in a tile that take the rest of their budget at once
 constexpr double kTileStarveGain = 0.0;  // margin growth per idle wave of the block at a record
@@ -132,8 +133,9 @@ struct AdaptTune {
   double tile_mstep;     // tiles: margin growth per batch (< 0: default)
   int tile_tail;         // tiles: pixels left that take the rest of their budget (< 0: default)
   double tile_starve;    // tiles: margin growth per idle wave of the block at a record (< 0: default)
+  int tile_split;        // tiles: predicted samples above this are split into two batches (0: default; huge: never)
 };
-static AdaptTune g_tune{0, 0, 0.0, 0, 0, 0, 0, 0, -1.0, -1, -1.0};
+static AdaptTune g_tune{0, 0, 0.0, 0, 0, 0, 0, 0, -1.0, -1, -1.0, 0};
 struct AdaptWs {
   DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer, [134] TileArgs
   DevBuf segs;                                  // counting renders: each slot's path segments (u16)
@@ -811,9 +813,9 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   if (tiles) {
     kcap = std::max(1, std::min(budget, g_tune.tile_kcap > 0 ? g_tune.tile_kcap : kTileKcap));
     // within the allowance: a pixel's batches get smaller, not the launch
-    const int64_t per_k = max_blocks * ntl * tp * (int64_t)(3 * sizeof(double) + (L.count ? 2 : 0));
+    const int64_t per_k = max_blocks * ntl * 2 * tp * (int64_t)(3 * sizeof(double) + (L.count ? 2 : 0));
     kcap = (int32_t)std::min<int64_t>(kcap, slot_target(sc, per_k, kcap, first_bytes));
-    const int64_t slots = max_blocks * ntl * tp * (int64_t)kcap;
+    const int64_t slots = max_blocks * ntl * 2 * tp * (int64_t)kcap;  // two batch buffers per tile
     if ((rc = w.lbuf.reserve(slots * 3 * sizeof(double)))) return rc;
     if (L.count && (rc = w.segs.reserve(slots * sizeof(uint16_t)))) return rc;
     for (DevBuf* b : {&w.k[0], &w.k[1], &w.off, &w.act})
@@ -848,6 +850,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   const double tile_mstep = g_tune.tile_mstep >= 0 ? g_tune.tile_mstep : kTileMarginStep;
   const int32_t tile_tail = g_tune.tile_tail >= 0 ? g_tune.tile_tail : kTileTail;
   const double tile_starve = g_tune.tile_starve >= 0 ? g_tune.tile_starve : kTileStarveGain;
+  const int32_t tile_split = g_tune.tile_split > 0 ? g_tune.tile_split : kTileSplit;
   unsigned long long* ctr = w.ctr.as<unsigned long long>();  // 8 region counters, then the slot count, ...
   const unsigned qb = (unsigned)((npix + kBlock - 1) / kBlock);
   // record + next batch sizes after phase g (its slots in Lph: the uniform first phase's, or the
@@ -940,7 +943,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ta.px = px, ta.npix = npix;
     ta.kcap = kcap, ta.min_spp = prm->min_spp, ta.budget = budget, ta.kinc = tile_kinc;
     ta.max_blocks = (int32_t)max_blocks, ta.k1 = std::min(K1, kcap);  // (a batch never exceeds kcap)
-    ta.tp = tp, ta.nt = ntl, ta.tail_px = tile_tail;
+    ta.tp = tp, ta.nt = ntl, ta.tail_px = tile_tail, ta.split = tile_split;
     ta.rel = prm->rel_threshold, ta.margin = tile_margin, ta.margin_step = tile_mstep, ta.starve_gain = tile_starve;
     hipLaunchKernelGGL(k_tile_setup, dim3(1), dim3(1), 0, s, ta, w.targs.as<TileArgs>(), ctr, rcn, (uint32_t)npix,
                        w.tcount.as<uint32_t>());
@@ -995,7 +998,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ta.px = px, ta.npix = npix;
     ta.kcap = kcap, ta.min_spp = prm->min_spp, ta.budget = budget, ta.kinc = tile_kinc;
     ta.max_blocks = (int32_t)max_blocks, ta.k1 = K1;
-    ta.tp = tp, ta.nt = ntl, ta.tail_px = tile_tail;
+    ta.tp = tp, ta.nt = ntl, ta.tail_px = tile_tail, ta.split = tile_split;
     ta.rel = prm->rel_threshold, ta.margin = tile_margin, ta.margin_step = tile_mstep, ta.starve_gain = tile_starve;
     hipLaunchKernelGGL(k_tile_setup, dim3(1), dim3(1), 0, s, ta, w.targs.as<TileArgs>(), ctr, RegionCounts{},
                        (uint32_t)npix, w.tcount.as<uint32_t>());
@@ -1948,13 +1951,13 @@ extern "C" int rtx_internal_check_sincos(int device, int64_t n, uint64_t seed, i
 // phases do (tests/test_gpu_timed.py runs the full budgets through forced small workspaces).
 extern "C" int rtx_internal_adapt_tune(int32_t tile_kcap, int32_t tile_kinc, double tile_margin, int64_t phase_slots,
                                        int32_t phase_kcap, int32_t tile_first_pass, int32_t tile_tp, int32_t tile_nt,
-                                       double tile_mstep, int32_t tile_tail, double tile_starve) {
+                                       double tile_mstep, int32_t tile_tail, double tile_starve, int32_t tile_split) {
   if (tile_kcap < 0 || tile_kinc < 0 || !(tile_margin >= 0) || phase_slots < 0 || phase_kcap < 0 ||
       tile_first_pass < 0 || tile_first_pass > 2 || tile_tp < 0 || tile_tp > kTileTP || tile_nt < 0 ||
-      tile_nt > kTileNT)
+      tile_nt > kTileNT || tile_split < 0)
     return fail(RTX_ERR_INVALID, "bad tuning value");
   g_tune = AdaptTune{tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap, tile_first_pass, tile_tp, tile_nt,
-                     tile_mstep, tile_tail, tile_starve};
+                     tile_mstep, tile_tail, tile_starve, tile_split};
   return RTX_OK;
 }
 

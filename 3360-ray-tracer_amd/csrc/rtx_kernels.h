@@ -140,8 +140,8 @@ struct PersistLds {
 // release / acquire), so no cross-XCD visibility is needed.  Largest tiles first keeps the
 // launch's end short: the last tiles claimed are the cheapest.
 // ---------------------------------------------------------------------------------------
-constexpr int kTileTP = 32;  // most pixels per tile (the record runs one lane per pixel; TileArgs::tp)
-constexpr int kTileNT = 16;  // most tiles in flight per workgroup (TileArgs::nt)
+constexpr int kTileTP = 16;  // most pixels per tile (the record runs one lane per pixel; TileArgs::tp)
+constexpr int kTileNT = 8;   // most tiles in flight per workgroup (TileArgs::nt)
 struct PixelSoA {
   double *sum, *mean, *m2;  // 3 x npix each (channel-major)
   int32_t* samples;
@@ -153,9 +153,9 @@ struct TileArgs {
   const uint32_t* act;     // subset pixels still sampling after the first pass, in image order
   const uint32_t* order;   // tile ids (tile t = act[t * tp ...]) in claim order, region by region
   const uint32_t* rcount;  // tiles of each of the 8 regions
-  const uint32_t* knext;   // each pixel's first batch (k_adapt_record of the first pass)
+  const uint32_t* knext;   // each pixel's predicted further samples (k_adapt_record of the first pass)
   const uint32_t* nact;    // the number of active pixels
-  double* L;               // radiance: tp * kcap slots per (block, descriptor)
+  double* L;               // radiance: two batches of tp * kcap slots per (block, descriptor)
   uint16_t* segs;          // counting builds: each slot's path segments (same indexing), else null
   unsigned long long* rec_segs;  // counting builds: segments of the recorded samples
   PixelSoA px;
@@ -168,33 +168,50 @@ struct TileArgs {
                        // image order, first batch k1 = min_spp samples; order and knext unused)
   int32_t tp, nt;      // pixels per tile (<= kTileTP), tiles in flight per workgroup (<= kTileNT)
   int32_t tail_px;     // a tile with at most this many pixels left sampling gives them the rest of
-                       // their budget (within kcap) in one batch: no further phase chains
-  int32_t pad_;
+                       // their budget (within kcap): no further phase chains
+  int32_t split;       // a pixel's predicted samples are traced as two batches (front, back) when
+                       // there are more than this many
   double rel, margin;
   double margin_step;  // the margin grows by this much with every batch of the tile
   double starve_gain;  // ... and by this much per wave of the block idle at the record (no work to claim)
 };
-// A tile in flight (LDS).  word = (cursor << 32) | T: the batch's T slots are claimed by
-// adding to the cursor (an add returns the phase's T with it, so a claim is consistent even
-// when it races the record that starts the next batch); rem counts the batch's paths still
-// running; slot s of the batch is sample s0[i] + (s - off[i]) of pixel pix[i], off[i] <= s <
-// off[i + 1].  state: 0 free, 1 being initialised, 2 in flight.
-struct TileDesc {
+// A tile in flight (LDS).  Its pixels' predicted samples are traced as two pipelined batches in
+// two buffers: the FRONT batch (recorded next, in sample order) and the BACK batch (the samples
+// that follow, laid out once the front's slots are all claimed), so the block traces the back
+// batch while the front's last paths finish instead of waiting for the front's record.  A
+// buffer: word = (cursor << 32) | T: its T slots are claimed by adding to the cursor (an add
+// returns T with it, so a claim is consistent even when it races a re-layout); rem counts its
+// paths still running; slot s is sample s0[i] + (s - off[i]) of pixel pix[i], off[i] <= s <
+// off[i + 1].
+struct TileBuf {
   unsigned long long word;
-  uint32_t rem, state, npx, phase;
+  uint32_t rem, pad_;
   uint32_t off[kTileTP + 1];
-  uint32_t pix[kTileTP];
   uint32_t s0[kTileTP];
   uint32_t pad2_;
 };
+struct TileDesc {
+  TileBuf b[2];
+  uint32_t state;  // 0 free, 1 being initialised, 2 in flight
+  uint32_t npx, phase;
+  uint32_t front;  // the front buffer (0 / 1)
+  uint32_t back;   // the back buffer: 0 not laid out, 1 laid out
+  uint32_t done;   // bit b: buffer b's batch has ended (its last path counted off), not yet recorded
+  uint32_t lock;   // the record and the back layout hold it
+  uint32_t haspred;  // some pixel has predicted samples beyond the front batch
+  uint32_t pix[kTileTP];
+  uint32_t pred[kTileTP];  // a pixel's predicted samples beyond the front batch; kTileDone: finished
+};
+constexpr uint32_t kTileDone = 0xFFFFFFFFu;
 struct TileLds {
-  uint32_t ready;      // descriptors whose batch has ended (to be recorded)
+  uint32_t ready;      // descriptors one of whose batches has ended (their records are due)
   uint32_t exhausted;  // the claim order is used up
   uint32_t idle;       // waves of the block waiting for work (no path, nothing to claim)
   uint32_t pad_;
   TileDesc d[kTileNT];
 };
-static_assert(sizeof(TileDesc) % 8 == 0 && sizeof(TileLds) % 8 == 0, "8-byte aligned tile descriptors");
+static_assert(sizeof(TileBuf) % 8 == 0 && sizeof(TileDesc) % 8 == 0 && sizeof(TileLds) % 8 == 0,
+              "8-byte aligned tile descriptors");
 
 // PARK: 0 the plain schedule, 1 the PARK schedule with the leaf-step walk (trace4_run_step),
 // 2 the PARK schedule with the speculative walk (trace4_run_spec; trees of at most
@@ -459,11 +476,11 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   }
   return v;
 }
-// A pixel's next batch once its batch is recorded and it is neither converged nor out of
-// budget: IsConverged holds at n samples once n >= var / (rel * max(|mean|, 1e-3))^2 in every
-// channel, so the batch is that many more samples (times the margin), at least kinc, within
-// the budget and the workspace.  Only the amount of work depends on it, never the result: a
-// sample traced past the pixel's convergence point is discarded by the record.
+// A pixel's predicted further samples once a batch is recorded and it is neither converged nor
+// out of budget: IsConverged holds at n samples once n >= var / (rel * max(|mean|, 1e-3))^2 in
+// every channel, so that many more samples (times the margin), at least kinc, within the budget
+// and the workspace.  Only the amount of work depends on it, never the result: a sample traced
+// past the pixel's convergence point is discarded by the record.
 __device__ __forceinline__ uint32_t tile_next_batch(const PixRec& r, const TileArgs* ta, uint32_t phase, uint32_t idle) {
   const double rel = ta->rel;
   double need = 0.0;
@@ -476,14 +493,45 @@ __device__ __forceinline__ uint32_t tile_next_batch(const PixRec& r, const TileA
   const double want = (need - (double)r.n) * (ta->margin + ta->margin_step * (double)phase + ta->starve_gain * (double)idle);
   int k = (want < (double)left) ? (int)ceil(want) : left;  // NaN / inf: the whole budget
   k = max(k, min(ta->kinc, left));
-  return (uint32_t)min(k, min(left, ta->kcap));
+  return (uint32_t)min(k, left);
 }
-// Slot index of the tile workspace: descriptor j of this block, batch slot s.
-__device__ __forceinline__ uint64_t tile_slot(const TileArgs* ta, int j, uint32_t s) {
-  return ((uint64_t)(blockIdx.x * (uint32_t)ta->nt + (uint32_t)j) * (uint32_t)ta->tp) * (uint64_t)ta->kcap + s;
+// The front share of a pixel's predicted samples kt (the rest goes to the back batch).
+__device__ __forceinline__ uint32_t tile_front_share(uint32_t kt, const TileArgs* ta) {
+  const uint32_t f = kt > (uint32_t)ta->split ? (kt + 1u) / 2u : kt;
+  return min(f, (uint32_t)ta->kcap);
+}
+// Slot index of the tile workspace: descriptor j of this block, buffer b, batch slot s.
+__device__ __forceinline__ uint64_t tile_slot(const TileArgs* ta, int j, int b, uint32_t s) {
+  return ((uint64_t)((blockIdx.x * (uint32_t)ta->nt + (uint32_t)j) * 2u + (uint32_t)b) * (uint32_t)ta->tp) *
+             (uint64_t)ta->kcap + s;
+}
+// Lays out buffer b of descriptor d: pixel i takes k samples from sample s (wave-uniform; the
+// whole wave; lanes >= npx pass k = 0).  Returns the batch's slot count.
+__device__ __forceinline__ uint32_t tile_layout(TileDesc& d, int b, int npx, uint32_t k, uint32_t s) {
+  const int i = (int)lane_id();
+  const uint32_t inc = wave_incl_scan(k);
+  const uint32_t T = __shfl(inc, 63);
+  TileBuf& B = d.b[b];
+  if (i < npx) B.off[i] = inc - k, B.s0[i] = s;
+  if (i == 0) B.off[npx] = T, B.rem = T;
+  return T;
+}
+__device__ __forceinline__ void tile_publish(TileBuf& B, uint32_t T) {
+  // the layout (LDS) and every statistic (global) complete before the slots are claimable
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane_id() == 0) atomicExch(&B.word, (unsigned long long)T);
+}
+__device__ __forceinline__ void tile_lock(TileDesc& d) {
+  if (lane_id() == 0)
+    while (atomicCAS(&d.lock, 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+__device__ __forceinline__ void tile_unlock(TileDesc& d) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane_id() == 0) atomicExch(&d.lock, 0u);
 }
 // Claims a free descriptor and the next tile in claim order (this block's region first, then
-// the others) and lays out the tile's first batch (wave-uniform; the whole wave).  false: no
+// the others) and lays out the tile's front batch (wave-uniform; the whole wave).  false: no
 // free descriptor, or the claim order is used up (then tl->exhausted is set).
 __device__ __forceinline__ bool tile_claim(TileLds* tl, const TileArgs* ta, unsigned long long* ctr, uint32_t region) {
   int j = -1;
@@ -520,64 +568,108 @@ __device__ __forceinline__ bool tile_claim(TileLds* tl, const TileArgs* ta, unsi
   const uint32_t first = (uint32_t)tid * (uint32_t)ta->tp, nact = *ta->nact;
   const int n = (int)min<uint32_t>((uint32_t)ta->tp, nact - first);
   const int i = (int)lane_id();
-  uint32_t p = 0, k = 0, s = 0;
+  uint32_t p = 0, kt = 0, s = 0;
   if (i < n) {
-    if (ta->act) p = ta->act[first + i], k = ta->knext[p];
-    else p = first + (uint32_t)i, k = (uint32_t)ta->k1;
+    if (ta->act) p = ta->act[first + i], kt = ta->knext[p];
+    else p = first + (uint32_t)i, kt = (uint32_t)ta->k1;
     s = (uint32_t)ta->px.samples[p];
   }
-  const uint32_t inc = wave_incl_scan(k);
-  const uint32_t T = __shfl(inc, 63);
-  if (i < n) d.pix[i] = p, d.s0[i] = s, d.off[i] = inc - k;
-  if (i == 0) d.off[n] = T, d.npx = (uint32_t)n, d.rem = T, d.phase = 0;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // the layout before the claim word
+  // the first pass of a one-launch render is not split: nothing is predicted before it
+  const uint32_t f = ta->act ? tile_front_share(kt, ta) : kt;
+  if (i < n) d.pix[i] = p, d.pred[i] = kt - f;
+  const uint32_t T = tile_layout(d, 0, n, f, s);
+  const bool hp = __ballot(i < n && kt > f) != 0;
   if (i == 0) {
-    atomicExch(&d.word, (unsigned long long)T);
-    atomicExch(&d.state, T ? 2u : 0u);  // (an active pixel always has a batch)
+    d.npx = (uint32_t)n, d.phase = 0, d.front = 0, d.back = 0, d.done = 0, d.lock = 0, d.haspred = hp ? 1u : 0u;
+    d.b[1].word = 0ull, d.b[1].rem = 0u;
   }
+  tile_publish(d.b[0], T);
+  if (i == 0) atomicExch(&d.state, T ? 2u : 0u);  // (an active pixel always has a batch)
   return T != 0;
 }
-// The batch of descriptor j has ended: replay it into the pixels' statistics (lane i = pixel
-// i of the tile) and lay out the next batch (wave-uniform; the whole wave).
+// The back batch of descriptor j once its front batch's slots are all claimed: each pixel's
+// predicted samples beyond the front batch, from the sample after the front batch's last
+// (wave-uniform; the whole wave; under the descriptor's lock, taken by the caller).
+__device__ __forceinline__ void tile_layout_back(TileDesc& d, const TileArgs* ta) {
+  const int i = (int)lane_id(), n = (int)d.npx, fb = (int)d.front, bb = fb ^ 1;
+  uint32_t k = 0, s = 0;
+  if (i < n) {
+    const uint32_t pr = d.pred[i];
+    if (pr != kTileDone) {
+      k = min(pr, (uint32_t)ta->kcap);  // (a buffer holds kcap samples of a pixel)
+      s = d.b[fb].s0[i] + (d.b[fb].off[i + 1] - d.b[fb].off[i]);
+      d.pred[i] = pr - k;
+    }
+  }
+  const uint32_t T = tile_layout(d, bb, n, k, s);
+  const bool hp = __ballot(i < n && d.pred[i] != kTileDone && d.pred[i] != 0u) != 0;
+  if (i == 0) d.haspred = hp ? 1u : 0u, d.back = 1u;
+  tile_publish(d.b[bb], T);
+}
+// Records the front batch of descriptor j while it has ended: replay it into the pixels'
+// statistics (lane i = pixel i of the tile), then the back batch becomes the front, or the next
+// front batch is laid out (wave-uniform; the whole wave).
 template <bool COUNT>
 __device__ __forceinline__ void tile_record(TileLds* tl, const TileArgs* ta, int j) {
   TileDesc& d = tl->d[j];
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // every lane's radiance store, before its count-off
+  tile_lock(d);
   const int i = (int)lane_id();
   const int n = (int)d.npx;
-  const uint32_t idle = *(volatile uint32_t*)&tl->idle;
-  uint32_t kn = 0, nrec = 0;
-  if (i < n) {
-    const uint32_t p = d.pix[i], o0 = d.off[i], K = d.off[i + 1] - o0;
-    PixRec r;
-    load_pixel(r, ta->px, ta->npix, p);
-    const int n0 = r.n;
-    if (K > 0) {
-      const uint64_t base = tile_slot(ta, j, o0);
-      replay_pixel<2>(r, ta->L + 3 * base, (int)K, ta->min_spp, ta->rel);
-      if (COUNT) {  // the segments of the samples recorded (the rest are discarded)
-        unsigned long long t = 0;
-        for (int k = 0; k < r.n - n0; k++) t += ta->segs[base + k];
-        atomicAdd(ta->rec_segs, t);
+  while (true) {
+    const int fb = (int)d.front, bb = fb ^ 1;
+    uint32_t old = 0;
+    if (i == 0) old = atomicAnd(&d.done, ~(1u << fb));
+    old = __shfl(old, 0);
+    if (!(old & (1u << fb))) break;  // the front batch is still running
+    const uint32_t idle = *(volatile uint32_t*)&tl->idle;
+    const bool back = d.back != 0u;
+    uint32_t kt = 0, nrec = 0;
+    bool live = false;  // the pixel is still sampling after this batch
+    if (i < n && d.pred[i] != kTileDone) {
+      const uint32_t p = d.pix[i], o0 = d.b[fb].off[i], K = d.b[fb].off[i + 1] - o0;
+      PixRec r;
+      load_pixel(r, ta->px, ta->npix, p);
+      const int n0 = r.n;
+      if (K > 0) {
+        const uint64_t base = tile_slot(ta, j, fb, o0);
+        replay_pixel<2>(r, ta->L + 3 * base, (int)K, ta->min_spp, ta->rel);
+        if (COUNT) {  // the segments of the samples recorded (the rest are discarded)
+          unsigned long long t = 0;
+          for (int k = 0; k < r.n - n0; k++) t += ta->segs[base + k];
+          atomicAdd(ta->rec_segs, t);
+        }
+        store_pixel(r, ta->px, ta->npix, p);
       }
-      store_pixel(r, ta->px, ta->npix, p);
-      if (!r.conv && r.n < ta->budget) kn = tile_next_batch(r, ta, d.phase, idle);
+      live = !r.conv && r.n < ta->budget;
+      if (live) kt = tile_next_batch(r, ta, d.phase, idle);
+      nrec = (uint32_t)r.n;
     }
-    nrec = (uint32_t)r.n;
+    // few pixels left sampling: the rest of their budget now, rather than more phases of a few paths
+    if ((int)__popcll(__ballot(live)) <= ta->tail_px && live) kt = (uint32_t)(ta->budget - (int)nrec);
+    if (back) {
+      // the back batch becomes the front: a live pixel's back samples follow the ones just
+      // recorded; the rest of its prediction waits for the next back batch
+      uint32_t kb = 0;
+      if (i < n) kb = d.b[bb].off[i + 1] - d.b[bb].off[i];
+      if (i < n && d.pred[i] != kTileDone) d.pred[i] = live ? (kt > kb ? kt - kb : 0u) : kTileDone;
+      const bool hp = __ballot(i < n && live && kt > kb) != 0;
+      if (i == 0) d.front = (uint32_t)bb, d.back = 0u, d.haspred = hp ? 1u : 0u, d.phase = d.phase + 1u;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      continue;  // the new front may have ended already
+    }
+    // no back batch: the next front batch now, in the other buffer
+    const uint32_t f = live ? tile_front_share(kt, ta) : 0u;
+    if (i < n && d.pred[i] != kTileDone) d.pred[i] = live ? kt - f : kTileDone;
+    const uint32_t T = tile_layout(d, bb, n, f, nrec);
+    const bool hp = __ballot(i < n && live && kt > f) != 0;
+    if (i == 0) d.front = (uint32_t)bb, d.back = 0u, d.haspred = hp ? 1u : 0u, d.phase = d.phase + 1u;
+    tile_publish(d.b[bb], T);
+    if (T == 0) {  // every pixel of the tile is finished
+      if (i == 0) atomicExch(&d.state, 0u);
+      break;
+    }
   }
-  // few pixels left sampling: the rest of their budget now, rather than more phases of a few paths
-  if ((int)__popcll(__ballot(kn != 0)) <= ta->tail_px && kn != 0)
-    kn = (uint32_t)min(ta->budget - (int)nrec, ta->kcap);
-  const uint32_t inc = wave_incl_scan(kn);
-  const uint32_t T = __shfl(inc, 63);
-  if (i < n) d.off[i] = inc - kn, d.s0[i] = nrec;
-  if (i == 0) d.off[n] = T, d.rem = T, d.phase = d.phase + 1;
-  // the statistics (global) and the layout (LDS) complete before the next batch is claimable
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if (i == 0) {
-    atomicExch(&d.word, (unsigned long long)T);
-    if (T == 0) atomicExch(&d.state, 0u);  // the tile is finished
-  }
+  tile_unlock(d);
 }
 // The wave's exit test: no tile left to claim, none in flight.
 __device__ __forceinline__ bool tiles_done(const TileLds* tl) {
@@ -679,25 +771,49 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
     constexpr int kRefill = kPark ? kRefillMinPark : kRefillMin;
     if (kTiles) {
       // tile schedule: the idle lanes take slots of the block's tiles in flight (descriptor
-      // order), one LDS add per tile; when those run out, the wave claims the next tile
+      // order; each tile's front batch, then its back batch, laid out here once the front's
+      // slots are all claimed), one LDS add per batch; when those run out, the wave claims the
+      // next tile
       if (idle != 0 && (__popcll(idle) >= kRefill || idle == ~0ull)) {
         const uint32_t nidle = (uint32_t)__popcll(idle);
         const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane_id()) - 1ull));
         uint32_t given = 0;
         const int nt = ta->nt;
         for (int j = 0; j < nt && given < nidle; j++) {
-          const unsigned long long w = *(volatile unsigned long long*)&tl->d[j].word;
-          const uint32_t wc = __builtin_amdgcn_readfirstlane((uint32_t)(w >> 32));
-          const uint32_t wt = __builtin_amdgcn_readfirstlane((uint32_t)w);
-          if (wc >= wt) continue;
-          unsigned long long old = 0;
-          if (lane_id() == 0) old = atomicAdd(&tl->d[j].word, (unsigned long long)(nidle - given) << 32);
-          const uint32_t c0 = __builtin_amdgcn_readfirstlane((uint32_t)(old >> 32));
-          const uint32_t T = __builtin_amdgcn_readfirstlane((uint32_t)old);
-          if (c0 >= T) continue;
-          const uint32_t got = min(nidle - given, T - c0);
-          if (!has && rank >= given && rank < given + got) slot = ((uint32_t)j << 24) | (c0 + rank - given), fresh = true;
-          given += got;
+          TileDesc& d = tl->d[j];
+          if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&d.state) != 2u) continue;
+          for (int h = 0; h < 2 && given < nidle; h++) {
+            const int b = (int)(__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&d.front) ^ (uint32_t)h);
+            const unsigned long long w = *(volatile unsigned long long*)&d.b[b].word;
+            const uint32_t wc = __builtin_amdgcn_readfirstlane((uint32_t)(w >> 32));
+            const uint32_t wt = __builtin_amdgcn_readfirstlane((uint32_t)w);
+            if (wc >= wt) {
+              // the front batch's slots are all claimed: lay out the back batch (once)
+              if (h == 0 && __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&d.haspred) &&
+                  !__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&d.back)) {
+                uint32_t got = 0;
+                if (lane_id() == 0) got = atomicCAS(&d.lock, 0u, 1u) == 0u ? 1u : 0u;
+                if (__builtin_amdgcn_readfirstlane(got)) {
+                  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                  const int fb = (int)d.front;
+                  const unsigned long long wf = *(volatile unsigned long long*)&d.b[fb].word;
+                  if (__builtin_amdgcn_readfirstlane(d.haspred && !d.back && (uint32_t)(wf >> 32) >= (uint32_t)wf ? 1u : 0u))
+                    tile_layout_back(d, ta);
+                  tile_unlock(d);
+                }
+              }
+              continue;
+            }
+            unsigned long long old = 0;
+            if (lane_id() == 0) old = atomicAdd(&d.b[b].word, (unsigned long long)(nidle - given) << 32);
+            const uint32_t c0 = __builtin_amdgcn_readfirstlane((uint32_t)(old >> 32));
+            const uint32_t T = __builtin_amdgcn_readfirstlane((uint32_t)old);
+            if (c0 >= T) continue;
+            const uint32_t got = min(nidle - given, T - c0);
+            if (!has && rank >= given && rank < given + got)
+              slot = ((uint32_t)j << 24) | ((uint32_t)b << 23) | (c0 + rank - given), fresh = true;
+            given += got;
+          }
         }
         if (given < nidle && !__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&tl->exhausted))
           tile_claim(tl, ta, next_slot, region);  // its slots go to the next refill
@@ -760,16 +876,17 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
       // nslots < 2^32 (checked on the host): 32-bit division
       uint2 e = make_uint2(0u, 0u);
       if (MAP == 1) e = ((const uint2*)next_slot[8 * 16 + 2])[slot];
-      if (kTiles) {  // batch slot s of descriptor j: the last pixel i with off[i] <= s
+      if (kTiles) {  // slot s of buffer b of descriptor j: the last pixel i with off[i] <= s
         const TileDesc& d = tl->d[slot >> 24];
-        const uint32_t s = slot & 0xFFFFFFu;
+        const TileBuf& B = d.b[(slot >> 23) & 1u];
+        const uint32_t s = slot & 0x7FFFFFu;
         int lo = 0, hi = (int)d.npx;
         while (hi - lo > 1) {
           const int mid = (lo + hi) >> 1;
-          if (d.off[mid] <= s) lo = mid;
+          if (B.off[mid] <= s) lo = mid;
           else hi = mid;
         }
-        e = make_uint2(d.pix[lo], d.s0[lo] + (s - d.off[lo]));
+        e = make_uint2(d.pix[lo], B.s0[lo] + (s - B.off[lo]));
       }
       const uint32_t p = MAP ? e.x : (uint32_t)slot / (uint32_t)Ar.K;
       if (kTiles || !(Ar.conv && Ar.conv[p])) {  // (a tile slot is always traced: its count-off ends the batch)
@@ -887,13 +1004,16 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
         // the radiance record, then the path is counted off its tile's batch; the count-off
         // that ends the batch marks the tile for its record (by a wave of this block: the
         // workgroup-scope release orders the store before the LDS count)
-        const int j = (int)(slot >> 24);
-        const uint64_t q = tile_slot(ta, j, slot & 0xFFFFFFu);
+        const int j = (int)(slot >> 24), b = (int)((slot >> 23) & 1u);
+        const uint64_t q = tile_slot(ta, j, b, slot & 0x7FFFFFu);
         double* Lq = ta->L + 3 * q;
         Lq[0] = L.x, Lq[1] = L.y, Lq[2] = L.z;
         if (COUNT) segbuf[q] = (uint16_t)min(pseg, 65535u);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (atomicSub(&tl->d[j].rem, 1u) == 1u) atomicOr(&tl->ready, 1u << j);
+        if (atomicSub(&tl->d[j].b[b].rem, 1u) == 1u) {
+          atomicOr(&tl->d[j].done, 1u << b);
+          atomicOr(&tl->ready, 1u << j);
+        }
       } else {
         store_radiance(A, slot, L);
         if (COUNT && segbuf) segbuf[slot] = (uint16_t)min(pseg, 65535u);

@@ -524,9 +524,22 @@ def cpu_baseline(rtx, dev, host, cam, preset, scene_name, spp, depth, args, park
                 "ratio_port_over_reference": r, "case": case["config"], "threads": c["threads"],
                 "where": c["host"], "reference_mrays_s": case["reference"]["mrays_s"],
                 "port_mrays_s": case["port"]["mrays_s"],
+                "reference_parallel": c.get("reference_parallel", "IntersectBatch only"),
                 "reference_equivalent_value": base["value"] / r,
-                "note": "port and reference (its own sources, oracle/_ref) timed on identical configs and threads; "
-                        "reference_equivalent_value = value / ratio estimates the reference on these cores"}
+                "note": "port and reference (its own sources, oracle/_ref) timed on identical configs and threads, the "
+                        "reference's shading loop parallel as wavefront.cc:105-217 runs it; reference_equivalent_value "
+                        "= value / ratio estimates the reference on these cores"}
+            # the same harness with the reference's shading loop run serially: on this host the
+            # reference is faster so (its OpenMP shading loop costs more than it gains), a
+            # conservative second estimate
+            ser = os.path.join(ROOT, "profiles", f"cpu_calibration_{threads}t_serial_shading.json")
+            if os.path.exists(ser):
+                sc = json.load(open(ser))["cases"].get(CALIBRATION_CASE.get(scene_name, ""))
+                if sc:
+                    base["calibration"]["serial_shading"] = {
+                        "ratio_port_over_reference": sc["ratio_port_over_reference"],
+                        "reference_mrays_s": sc["reference"]["mrays_s"],
+                        "reference_equivalent_value": base["value"] / sc["ratio_port_over_reference"]}
     check = {"mode": args.mode, "precision": args.precision, "schedule": sched,
              "kernel_build": rtx.build_names(gst["build"]), "same_build_as_timed": gst["build"] == build_bits,
              "rows": [tile[1], tile[1] + tile[3]],

@@ -1,0 +1,23 @@
+#!/bin/bash
+# Round 4: the tile schedule with pipelined (front / back) batches: parity first, then C3
+# adaptive sweeps of its knobs beside the phase schedule.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/r5f; mkdir -p $O
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py \
+  -k "adaptive_schedules or group_size or persistent_schedule_equals" > $O/pytest_parity.log 2>&1 || exit 1
+B="--adaptive --steps 6 --warmup 1 --no-cpu-baseline --no-generic-leg"
+run() {  # tag, extra args
+  timeout -k 10 120 python bench.py $B $2 > $O/sweep_$1.json 2> $O/sweep_$1.err || exit 1
+  python3 scripts/sweep_summary.py $1 $O/sweep_$1.json >> $O/sweep.txt
+}
+run phases "--adapt-schedule phases"
+run default ""
+for t in tile_split=1000000 tile_split=16 tile_split=4 tile_tp=4 tile_tp=16 tile_nt=4 tile_starve=0.5 \
+         tile_margin=1.25 tile_kinc=16 tile_tail=2 tile_first_pass=1; do
+  run "$t" "--adapt-tune $t"
+done
+cat $O/sweep.txt
+timeout -k 10 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_timed.py \
+  -k "adaptive" > $O/pytest_timed.log 2>&1 || exit 1
+echo done

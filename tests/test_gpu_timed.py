@@ -160,6 +160,7 @@ TUNES = {"tiles": ({}, False), "tiles_small": (dict(tile_kcap=8, tile_kinc=4, ti
          "tiles_one": (dict(tile_kcap=1, tile_kinc=1), False), "phases": ({}, True),
          "tiles_one_launch": (dict(tile_first_pass=1), False),
          "tiles_one_launch_small": (dict(tile_first_pass=1, tile_kcap=8, tile_kinc=4), False),
+         "tiles_split2_kcap5": (dict(tile_split=2, tile_kcap=5, tile_tp=3, tile_nt=3), False),
          "phases_small": (dict(phase_slots=4096, phase_kcap=8), True)}
 
 
