@@ -916,6 +916,14 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
         uint32_t tc[9] = {};
         HIPC(hipMemcpy(tc, w.tcount.p, sizeof tc, hipMemcpyDeviceToHost));
         pixels = tc[8];
+        unsigned long long tt[18] = {};
+        HIPC(hipMemcpy(tt, A.counters, sizeof tt, hipMemcpyDeviceToHost));
+        if (tt[13]) {  // counting build: the tile launch's timeline (us from the first block's start)
+          const double t0 = (double)~tt[13];
+          auto us = [&](unsigned long long v) { return ((double)v - t0) / 100.0; };
+          fprintf(stderr, "rtx adaptive: tiles timeline: claim order used up %.1f .. %.1f us, waves end %.1f .. %.1f us\n",
+                  us(~tt[15]), us(tt[14]), us(~tt[17]), us(tt[16]));
+        }
       }
       fprintf(stderr, "rtx adaptive: %s %d: %lld pixels, launch %.3f ms, %llu segments (%.0f Mseg/s)\n",
               Lg.map == 2 ? "tiles after phase" : "phase", g, (long long)pixels, ms, seg1 - seg0,

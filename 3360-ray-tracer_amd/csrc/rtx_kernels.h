@@ -533,7 +533,8 @@ __device__ __forceinline__ void tile_unlock(TileDesc& d) {
 // Claims a free descriptor and the next tile in claim order (this block's region first, then
 // the others) and lays out the tile's front batch (wave-uniform; the whole wave).  false: no
 // free descriptor, or the claim order is used up (then tl->exhausted is set).
-__device__ __forceinline__ bool tile_claim(TileLds* tl, const TileArgs* ta, unsigned long long* ctr, uint32_t region) {
+__device__ __forceinline__ bool tile_claim(TileLds* tl, const TileArgs* ta, unsigned long long* ctr, uint32_t region,
+                                           unsigned long long* tstat = nullptr) {
   int j = -1;
   const int nt = ta->nt;
   if (lane_id() == 0)
@@ -560,6 +561,11 @@ __device__ __forceinline__ bool tile_claim(TileLds* tl, const TileArgs* ta, unsi
   TileDesc& d = tl->d[j];
   if (tid < 0) {
     if (lane_id() == 0) {
+      if (tstat && atomicExch(&tl->exhausted, 1u) == 0u) {  // (counting builds: the timeline)
+        const unsigned long long t = (unsigned long long)wall_clock64();
+        atomicMax(tstat + 14, t);
+        atomicMax(tstat + 15, ~t);
+      }
       atomicExch(&tl->exhausted, 1u);
       atomicExch(&d.state, 0u);
     }
@@ -713,6 +719,10 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   if (kTiles) {
     if (blockIdx.x >= (uint32_t)ta->max_blocks) return;  // (the host sizes the grid within it)
     for (uint32_t w = threadIdx.x; w < sizeof(TileLds) / 4; w += kBlock) ((uint32_t*)tl)[w] = 0u;
+    // counting builds: the launch's timeline (wall clock, 100 MHz): [13] ~first block start,
+    // [14] last block to find the claim order used up, [15] ~first one, [16] last wave end,
+    // [17] ~first wave end
+    if (COUNT && threadIdx.x == 0) atomicMax(&A.counters[13], ~(unsigned long long)wall_clock64());
     __syncthreads();
   }
   uint32_t* stk = (uint32_t*)(ldsb + lay.stack) + threadIdx.x;
@@ -816,7 +826,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
           }
         }
         if (given < nidle && !__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&tl->exhausted))
-          tile_claim(tl, ta, next_slot, region);  // its slots go to the next refill
+          tile_claim(tl, ta, next_slot, region, COUNT ? A.counters : nullptr);  // its slots go to the next refill
       }
     } else if (idle != 0 && !exhausted && (__popcll(idle) >= kRefill || idle == ~0ull)) {
       const uint64_t nidle = (uint64_t)__popcll(idle);
@@ -1022,6 +1032,11 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
     }
   }
   flush_counters(A, c, segs, prims, COUNT);
+  if (COUNT && kTiles && lane_id() == 0) {
+    const unsigned long long t = (unsigned long long)wall_clock64();
+    atomicMax(&A.counters[16], t);
+    atomicMax(&A.counters[17], ~t);
+  }
 }
 
 // The PARK instantiations are compiled in their own translation unit (rtx_park.hip), with
