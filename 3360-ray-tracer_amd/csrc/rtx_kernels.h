@@ -140,8 +140,8 @@ struct PersistLds {
 // release / acquire), so no cross-XCD visibility is needed.  Largest tiles first keeps the
 // launch's end short: the last tiles claimed are the cheapest.
 // ---------------------------------------------------------------------------------------
-constexpr int kTileTP = 16;  // most pixels per tile (the record runs one lane per pixel; TileArgs::tp)
-constexpr int kTileNT = 8;   // most tiles in flight per workgroup (TileArgs::nt)
+constexpr int kTileTP = 8;   // most pixels per tile (the record runs one lane per pixel; TileArgs::tp)
+constexpr int kTileNT = 10;  // most tiles in flight per workgroup (TileArgs::nt)
 struct PixelSoA {
   double *sum, *mean, *m2;  // 3 x npix each (channel-major)
   int32_t* samples;
@@ -177,12 +177,13 @@ struct TileArgs {
 };
 // A tile in flight (LDS).  Its pixels' predicted samples are traced as two pipelined batches in
 // two buffers: the FRONT batch (recorded next, in sample order) and the BACK batch (the samples
-// that follow, laid out once the front's slots are all claimed), so the block traces the back
+// that follow), both laid out at once, front first in claim order, so the block traces the back
 // batch while the front's last paths finish instead of waiting for the front's record.  A
 // buffer: word = (cursor << 32) | T: its T slots are claimed by adding to the cursor (an add
 // returns T with it, so a claim is consistent even when it races a re-layout); rem counts its
 // paths still running; slot s is sample s0[i] + (s - off[i]) of pixel pix[i], off[i] <= s <
-// off[i + 1].
+// off[i + 1].  Only the record (one wave at a time per tile: it claims the front's done bit)
+// lays out batches.
 struct TileBuf {
   unsigned long long word;
   uint32_t rem, pad_;
@@ -194,21 +195,23 @@ struct TileDesc {
   TileBuf b[2];
   uint32_t state;  // 0 free, 1 being initialised, 2 in flight
   uint32_t npx, phase;
-  uint32_t front;  // the front buffer (0 / 1)
-  uint32_t back;   // the back buffer: 0 not laid out, 1 laid out
+  uint32_t front;  // the front buffer (0 / 1); the other one holds the back batch
   uint32_t done;   // bit b: buffer b's batch has ended (its last path counted off), not yet recorded
-  uint32_t lock;   // the record and the back layout hold it
-  uint32_t haspred;  // some pixel has predicted samples beyond the front batch
+  uint32_t pad_;
   uint32_t pix[kTileTP];
-  uint32_t pred[kTileTP];  // a pixel's predicted samples beyond the front batch; kTileDone: finished
+  uint32_t fin[kTileTP];  // 1: the pixel is finished (converged or out of budget)
 };
 constexpr uint32_t kTileDone = 0xFFFFFFFFu;
 struct TileLds {
   uint32_t ready;      // descriptors one of whose batches has ended (their records are due)
   uint32_t exhausted;  // the claim order is used up
   uint32_t idle;       // waves of the block waiting for work (no path, nothing to claim)
-  uint32_t pad_;
+  uint32_t avail;      // bit 2 j + b: buffer b of descriptor j may have unclaimed slots
   TileDesc d[kTileNT];
+  // each wave's record keeps the pixels' statistics here (sum, mean, M2 by channel, pixel
+  // interleaved), not in registers: the record runs inside the persistent loop, where every
+  // register of the walk is taken
+  double rec[kBlock / 64][9][kTileTP];
 };
 static_assert(sizeof(TileBuf) % 8 == 0 && sizeof(TileDesc) % 8 == 0 && sizeof(TileLds) % 8 == 0,
               "8-byte aligned tile descriptors");
@@ -456,6 +459,46 @@ __device__ __forceinline__ void replay_pixel(PixRec& r, const double* __restrict
     }
   }
 }
+// replay_pixel's arithmetic, in the same order, on statistics held in LDS (st[q * kTileTP]: sum
+// 0-2, mean 3-5, M2 6-8, one column per pixel): the tile schedule's record inside the persistent
+// loop (volatile: every step reads and writes them, none is kept in a register).
+__device__ __forceinline__ void replay_pixel_lds(volatile double* st, int& n, bool& conv, const double* __restrict__ Lp,
+                                                 int K, int min_spp, double rel) {
+  constexpr int S = kTileTP;
+  for (int k = 0; k < K && !conv; k++) {
+    double x[3];
+    for (int c = 0; c < 3; c++) x[c] = Lp[3 * k + c];
+    n++;
+    for (int c = 0; c < 3; c++) {
+      double mu = st[(3 + c) * S];
+      double delta = x[c] - mu;
+      mu += delta / n;
+      double delta2 = x[c] - mu;
+      st[(3 + c) * S] = mu;
+      st[(6 + c) * S] = st[(6 + c) * S] + delta2 * delta;
+    }
+    for (int c = 0; c < 3; c++) st[c * S] = st[c * S] + x[c];
+    if (n >= min_spp) {
+      bool ok = true;
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        if (ok) {
+          const double m2 = st[(6 + c) * S];
+          double mu = fmax(fabs(st[(3 + c) * S]), 1e-3);
+          const double thr = rel * rel * ((double)(n - 1) * (double)n * (mu * mu));
+          if (m2 > thr * (1.0 + 1e-10)) {
+            ok = false;
+          } else if (!(m2 < thr * (1.0 - 1e-10))) {
+            double var = n > 1 ? m2 / (n - 1) : 0.0;
+            double err = sqrt(var) / sqrt((double)n);
+            if (err / mu > rel) ok = false;
+          }
+        }
+      }
+      conv = ok;
+    }
+  }
+}
 __device__ __forceinline__ void load_pixel(PixRec& r, const PixelSoA& px, int64_t npix, int64_t p) {
   for (int c = 0; c < 3; c++) r.sum[c] = px.sum[c * npix + p], r.mean[c] = px.mean[c * npix + p], r.m2[c] = px.m2[c * npix + p];
   r.n = px.samples[p];
@@ -505,34 +548,29 @@ __device__ __forceinline__ uint64_t tile_slot(const TileArgs* ta, int j, int b, 
   return ((uint64_t)((blockIdx.x * (uint32_t)ta->nt + (uint32_t)j) * 2u + (uint32_t)b) * (uint32_t)ta->tp) *
              (uint64_t)ta->kcap + s;
 }
-// Lays out buffer b of descriptor d: pixel i takes k samples from sample s (wave-uniform; the
-// whole wave; lanes >= npx pass k = 0).  Returns the batch's slot count.
-__device__ __forceinline__ uint32_t tile_layout(TileDesc& d, int b, int npx, uint32_t k, uint32_t s) {
+// Lays out buffer b of descriptor j: pixel i takes k samples from sample s, and publishes it
+// (wave-uniform; the whole wave; lanes >= npx pass k = 0).  A batch without slots is ended at
+// once (its done bit).  Returns the batch's slot count.
+__device__ __forceinline__ uint32_t tile_layout(TileLds* tl, int j, int b, int npx, uint32_t k, uint32_t s) {
+  TileDesc& d = tl->d[j];
   const int i = (int)lane_id();
   const uint32_t inc = wave_incl_scan(k);
   const uint32_t T = __shfl(inc, 63);
   TileBuf& B = d.b[b];
   if (i < npx) B.off[i] = inc - k, B.s0[i] = s;
   if (i == 0) B.off[npx] = T, B.rem = T;
-  return T;
-}
-__device__ __forceinline__ void tile_publish(TileBuf& B, uint32_t T) {
   // the layout (LDS) and every statistic (global) complete before the slots are claimable
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if (lane_id() == 0) atomicExch(&B.word, (unsigned long long)T);
-}
-__device__ __forceinline__ void tile_lock(TileDesc& d) {
-  if (lane_id() == 0)
-    while (atomicCAS(&d.lock, 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(1);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-__device__ __forceinline__ void tile_unlock(TileDesc& d) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  if (lane_id() == 0) atomicExch(&d.lock, 0u);
+  if (i == 0) {
+    atomicExch(&B.word, (unsigned long long)T);
+    if (T) atomicOr(&tl->avail, 1u << (2 * j + b));
+    else atomicOr(&d.done, 1u << b);
+  }
+  return T;
 }
 // Claims a free descriptor and the next tile in claim order (this block's region first, then
-// the others) and lays out the tile's front batch (wave-uniform; the whole wave).  false: no
-// free descriptor, or the claim order is used up (then tl->exhausted is set).
+// the others) and lays out its front and back batches (wave-uniform; the whole wave).  false:
+// no free descriptor, or the claim order is used up (then tl->exhausted is set).
 __device__ __forceinline__ bool tile_claim(TileLds* tl, const TileArgs* ta, unsigned long long* ctr, uint32_t region,
                                            unsigned long long* tstat = nullptr) {
   int j = -1;
@@ -582,43 +620,21 @@ __device__ __forceinline__ bool tile_claim(TileLds* tl, const TileArgs* ta, unsi
   }
   // the first pass of a one-launch render is not split: nothing is predicted before it
   const uint32_t f = ta->act ? tile_front_share(kt, ta) : kt;
-  if (i < n) d.pix[i] = p, d.pred[i] = kt - f;
-  const uint32_t T = tile_layout(d, 0, n, f, s);
-  const bool hp = __ballot(i < n && kt > f) != 0;
-  if (i == 0) {
-    d.npx = (uint32_t)n, d.phase = 0, d.front = 0, d.back = 0, d.done = 0, d.lock = 0, d.haspred = hp ? 1u : 0u;
-    d.b[1].word = 0ull, d.b[1].rem = 0u;
-  }
-  tile_publish(d.b[0], T);
+  if (i < n) d.pix[i] = p, d.fin[i] = 0u;
+  if (i == 0) d.npx = (uint32_t)n, d.phase = 0, d.front = 0, d.done = 0;
+  const uint32_t T = tile_layout(tl, j, 0, n, f, s);
+  tile_layout(tl, j, 1, n, min(kt - f, (uint32_t)ta->kcap), s + f);
   if (i == 0) atomicExch(&d.state, T ? 2u : 0u);  // (an active pixel always has a batch)
   return T != 0;
 }
-// The back batch of descriptor j once its front batch's slots are all claimed: each pixel's
-// predicted samples beyond the front batch, from the sample after the front batch's last
-// (wave-uniform; the whole wave; under the descriptor's lock, taken by the caller).
-__device__ __forceinline__ void tile_layout_back(TileDesc& d, const TileArgs* ta) {
-  const int i = (int)lane_id(), n = (int)d.npx, fb = (int)d.front, bb = fb ^ 1;
-  uint32_t k = 0, s = 0;
-  if (i < n) {
-    const uint32_t pr = d.pred[i];
-    if (pr != kTileDone) {
-      k = min(pr, (uint32_t)ta->kcap);  // (a buffer holds kcap samples of a pixel)
-      s = d.b[fb].s0[i] + (d.b[fb].off[i + 1] - d.b[fb].off[i]);
-      d.pred[i] = pr - k;
-    }
-  }
-  const uint32_t T = tile_layout(d, bb, n, k, s);
-  const bool hp = __ballot(i < n && d.pred[i] != kTileDone && d.pred[i] != 0u) != 0;
-  if (i == 0) d.haspred = hp ? 1u : 0u, d.back = 1u;
-  tile_publish(d.b[bb], T);
-}
 // Records the front batch of descriptor j while it has ended: replay it into the pixels'
-// statistics (lane i = pixel i of the tile), then the back batch becomes the front, or the next
-// front batch is laid out (wave-uniform; the whole wave).
+// statistics (lane i = pixel i of the tile); the back batch becomes the front, and the samples
+// predicted beyond it are laid out as the new back batch in the buffer just recorded
+// (wave-uniform; the whole wave; one wave per tile at a time: it claims the front's done bit).
 template <bool COUNT>
 __device__ __forceinline__ void tile_record(TileLds* tl, const TileArgs* ta, int j) {
   TileDesc& d = tl->d[j];
-  tile_lock(d);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // every lane's radiance store, before its count-off
   const int i = (int)lane_id();
   const int n = (int)d.npx;
   while (true) {
@@ -627,55 +643,71 @@ __device__ __forceinline__ void tile_record(TileLds* tl, const TileArgs* ta, int
     if (i == 0) old = atomicAnd(&d.done, ~(1u << fb));
     old = __shfl(old, 0);
     if (!(old & (1u << fb))) break;  // the front batch is still running
-    const uint32_t idle = *(volatile uint32_t*)&tl->idle;
-    const bool back = d.back != 0u;
-    uint32_t kt = 0, nrec = 0;
-    bool live = false;  // the pixel is still sampling after this batch
-    if (i < n && d.pred[i] != kTileDone) {
-      const uint32_t p = d.pix[i], o0 = d.b[fb].off[i], K = d.b[fb].off[i + 1] - o0;
-      PixRec r;
-      load_pixel(r, ta->px, ta->npix, p);
-      const int n0 = r.n;
-      if (K > 0) {
-        const uint64_t base = tile_slot(ta, j, fb, o0);
-        replay_pixel<2>(r, ta->L + 3 * base, (int)K, ta->min_spp, ta->rel);
-        if (COUNT) {  // the segments of the samples recorded (the rest are discarded)
-          unsigned long long t = 0;
-          for (int k = 0; k < r.n - n0; k++) t += ta->segs[base + k];
-          atomicAdd(ta->rec_segs, t);
+    if (__ballot(i < n && d.fin[i] == 0u) == 0) {
+      // every pixel is finished: the tile ends once the back batch has no path running
+      if (i == 0) {
+        if (old & (1u << bb)) {
+          atomicAnd(&d.done, ~(1u << bb));
+          atomicAnd(&tl->avail, ~(3u << (2 * j)));
+          atomicExch(&d.state, 0u);
+        } else {
+          atomicOr(&d.done, 1u << fb);  // (empty: the back's record finds it ended)
+          d.front = (uint32_t)bb;
         }
-        store_pixel(r, ta->px, ta->npix, p);
       }
-      live = !r.conv && r.n < ta->budget;
-      if (live) kt = tile_next_batch(r, ta, d.phase, idle);
-      nrec = (uint32_t)r.n;
-    }
-    // few pixels left sampling: the rest of their budget now, rather than more phases of a few paths
-    if ((int)__popcll(__ballot(live)) <= ta->tail_px && live) kt = (uint32_t)(ta->budget - (int)nrec);
-    if (back) {
-      // the back batch becomes the front: a live pixel's back samples follow the ones just
-      // recorded; the rest of its prediction waits for the next back batch
-      uint32_t kb = 0;
-      if (i < n) kb = d.b[bb].off[i + 1] - d.b[bb].off[i];
-      if (i < n && d.pred[i] != kTileDone) d.pred[i] = live ? (kt > kb ? kt - kb : 0u) : kTileDone;
-      const bool hp = __ballot(i < n && live && kt > kb) != 0;
-      if (i == 0) d.front = (uint32_t)bb, d.back = 0u, d.haspred = hp ? 1u : 0u, d.phase = d.phase + 1u;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      continue;  // the new front may have ended already
-    }
-    // no back batch: the next front batch now, in the other buffer
-    const uint32_t f = live ? tile_front_share(kt, ta) : 0u;
-    if (i < n && d.pred[i] != kTileDone) d.pred[i] = live ? kt - f : kTileDone;
-    const uint32_t T = tile_layout(d, bb, n, f, nrec);
-    const bool hp = __ballot(i < n && live && kt > f) != 0;
-    if (i == 0) d.front = (uint32_t)bb, d.back = 0u, d.haspred = hp ? 1u : 0u, d.phase = d.phase + 1u;
-    tile_publish(d.b[bb], T);
-    if (T == 0) {  // every pixel of the tile is finished
-      if (i == 0) atomicExch(&d.state, 0u);
       break;
     }
+    const uint32_t idle = *(volatile uint32_t*)&tl->idle;
+    const bool exh = *(volatile uint32_t*)&tl->exhausted != 0u;
+    uint32_t kt = 0, nrec = 0;
+    bool live = false;  // the pixel is still sampling after this batch
+    if (i < n && d.fin[i] == 0u) {
+      const uint32_t p = d.pix[i], o0 = d.b[fb].off[i], K = d.b[fb].off[i + 1] - o0;
+      const PixelSoA& px = ta->px;
+      const int64_t np = ta->npix;
+      volatile double* st = &tl->rec[threadIdx.x >> 6][0][i];
+      int nn = px.samples[p];
+      bool conv = false;
+      const int n0 = nn;
+      if (K > 0) {
+        for (int c = 0; c < 3; c++)
+          st[c * kTileTP] = px.sum[c * np + p], st[(3 + c) * kTileTP] = px.mean[c * np + p],
+          st[(6 + c) * kTileTP] = px.m2[c * np + p];
+        const uint64_t base = tile_slot(ta, j, fb, o0);
+        replay_pixel_lds(st, nn, conv, ta->L + 3 * base, (int)K, ta->min_spp, ta->rel);
+        if (COUNT) {  // the segments of the samples recorded (the rest are discarded)
+          unsigned long long t = 0;
+          for (int k = 0; k < nn - n0; k++) t += ta->segs[base + k];
+          atomicAdd(ta->rec_segs, t);
+        }
+        for (int c = 0; c < 3; c++)
+          px.sum[c * np + p] = st[c * kTileTP], px.mean[c * np + p] = st[(3 + c) * kTileTP],
+          px.m2[c * np + p] = st[(6 + c) * kTileTP];
+        px.samples[p] = nn;
+        px.conv[p] = conv;
+      }
+      live = !conv && nn < ta->budget;
+      if (live) {
+        PixRec r;  // (only what the prediction reads)
+        for (int c = 0; c < 3; c++) r.mean[c] = px.mean[c * np + p], r.m2[c] = px.m2[c * np + p];
+        r.n = nn;
+        kt = tile_next_batch(r, ta, d.phase, idle);
+      } else {
+        d.fin[i] = 1u;
+      }
+      nrec = (uint32_t)nn;
+    }
+    // few pixels left sampling, or nothing left to claim: the rest of their budget now, rather
+    // than further batches of a few paths each
+    if (live && (exh || (int)__popcll(__ballot(live)) <= ta->tail_px)) kt = (uint32_t)(ta->budget - (int)nrec);
+    // a live pixel's back samples follow the ones just recorded (nrec == its back batch's first
+    // sample); what its prediction wants beyond them goes in the new back batch
+    uint32_t kb = 0, sb = 0;
+    if (i < n) kb = d.b[bb].off[i + 1] - d.b[bb].off[i], sb = d.b[bb].s0[i];
+    const uint32_t kn = live ? min(kt > kb ? kt - kb : 0u, (uint32_t)ta->kcap) : 0u;
+    if (i == 0) d.front = (uint32_t)bb, d.phase = d.phase + 1u;
+    tile_layout(tl, j, fb, n, kn, sb + kb);
   }
-  tile_unlock(d);
 }
 // The wave's exit test: no tile left to claim, none in flight.
 __device__ __forceinline__ bool tiles_done(const TileLds* tl) {
@@ -788,41 +820,37 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
         const uint32_t nidle = (uint32_t)__popcll(idle);
         const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane_id()) - 1ull));
         uint32_t given = 0;
-        const int nt = ta->nt;
-        for (int j = 0; j < nt && given < nidle; j++) {
+        // descriptors with unclaimed slots (tl->avail: a hint; each buffer's word decides)
+        uint32_t av = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&tl->avail);
+        while (av != 0u && given < nidle) {
+          const int j = (int)(__builtin_ctz(av) >> 1);
+          av &= ~(3u << (2 * j));
           TileDesc& d = tl->d[j];
-          if (__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&d.state) != 2u) continue;
-          for (int h = 0; h < 2 && given < nidle; h++) {
+          for (int h = 0; h < 2 && given < nidle; h++) {  // the front batch first
             const int b = (int)(__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&d.front) ^ (uint32_t)h);
             const unsigned long long w = *(volatile unsigned long long*)&d.b[b].word;
             const uint32_t wc = __builtin_amdgcn_readfirstlane((uint32_t)(w >> 32));
             const uint32_t wt = __builtin_amdgcn_readfirstlane((uint32_t)w);
-            if (wc >= wt) {
-              // the front batch's slots are all claimed: lay out the back batch (once)
-              if (h == 0 && __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&d.haspred) &&
-                  !__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&d.back)) {
-                uint32_t got = 0;
-                if (lane_id() == 0) got = atomicCAS(&d.lock, 0u, 1u) == 0u ? 1u : 0u;
-                if (__builtin_amdgcn_readfirstlane(got)) {
-                  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                  const int fb = (int)d.front;
-                  const unsigned long long wf = *(volatile unsigned long long*)&d.b[fb].word;
-                  if (__builtin_amdgcn_readfirstlane(d.haspred && !d.back && (uint32_t)(wf >> 32) >= (uint32_t)wf ? 1u : 0u))
-                    tile_layout_back(d, ta);
-                  tile_unlock(d);
-                }
+            uint32_t c0 = wc, T = wt;
+            if (wc < wt) {
+              unsigned long long old = 0;
+              if (lane_id() == 0) old = atomicAdd(&d.b[b].word, (unsigned long long)(nidle - given) << 32);
+              c0 = __builtin_amdgcn_readfirstlane((uint32_t)(old >> 32));
+              T = __builtin_amdgcn_readfirstlane((uint32_t)old);
+              if (c0 < T) {
+                const uint32_t got = min(nidle - given, T - c0);
+                if (!has && rank >= given && rank < given + got)
+                  slot = ((uint32_t)j << 24) | ((uint32_t)b << 23) | (c0 + rank - given), fresh = true;
+                given += got;
+                c0 += got;
               }
-              continue;
             }
-            unsigned long long old = 0;
-            if (lane_id() == 0) old = atomicAdd(&d.b[b].word, (unsigned long long)(nidle - given) << 32);
-            const uint32_t c0 = __builtin_amdgcn_readfirstlane((uint32_t)(old >> 32));
-            const uint32_t T = __builtin_amdgcn_readfirstlane((uint32_t)old);
-            if (c0 >= T) continue;
-            const uint32_t got = min(nidle - given, T - c0);
-            if (!has && rank >= given && rank < given + got)
-              slot = ((uint32_t)j << 24) | ((uint32_t)b << 23) | (c0 + rank - given), fresh = true;
-            given += got;
+            if (c0 >= T && lane_id() == 0) {
+              // used up: clear the hint, then set it again if a record has re-laid the buffer
+              atomicAnd(&tl->avail, ~(1u << (2 * j + b)));
+              const unsigned long long w2 = *(volatile unsigned long long*)&d.b[b].word;
+              if ((uint32_t)(w2 >> 32) < (uint32_t)w2) atomicOr(&tl->avail, 1u << (2 * j + b));
+            }
           }
         }
         if (given < nidle && !__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&tl->exhausted))

@@ -249,7 +249,7 @@ def test_adaptive_schedules_equal_uniform_groups(rtx_mod, dev_scenes, scene, pre
             ("tiles_kcap4", dict(tile_kcap=4, tile_kinc=1, tile_margin=0.5), {}),
             ("tiles_one_launch_kcap3", dict(tile_kcap=3, tile_kinc=2, tile_first_pass=1), {}),
             ("tiles_no_split", dict(tile_split=1 << 30), {}), ("tiles_split1_tp1", dict(tile_split=1, tile_tp=1), {}),
-            ("tiles_tp16_nt2_tail", dict(tile_tp=16, tile_nt=2, tile_tail=3, tile_starve=1.0), {}),
+            ("tiles_tp8_nt2_tail", dict(tile_tp=8, tile_nt=2, tile_tail=3, tile_starve=1.0), {}),
             ("tiles_kcap3", dict(tile_kcap=3, tile_kinc=2, tile_margin=2.0), {}),
             ("phases", {}, dict(adapt_phases=True)),
             ("phases_small", dict(phase_slots=1024, phase_kcap=8), dict(adapt_phases=True))]
