@@ -524,16 +524,18 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
 // every channel, so that many more samples (times the margin), at least kinc, within the budget
 // and the workspace.  Only the amount of work depends on it, never the result: a sample traced
 // past the pixel's convergence point is discarded by the record.
-__device__ __forceinline__ uint32_t tile_next_batch(const PixRec& r, const TileArgs* ta, uint32_t phase, uint32_t idle) {
+// (st: the pixel's statistics in the record's LDS columns, as replay_pixel_lds keeps them)
+__device__ __forceinline__ uint32_t tile_next_batch(volatile const double* st, int n, const TileArgs* ta,
+                                                    uint32_t phase, uint32_t idle) {
   const double rel = ta->rel;
   double need = 0.0;
   for (int c = 0; c < 3; c++) {
-    const double var = r.n > 1 ? r.m2[c] / (r.n - 1) : 0.0;
-    const double mu = fmax(fabs(r.mean[c]), 1e-3);
+    const double var = n > 1 ? st[(6 + c) * kTileTP] / (n - 1) : 0.0;
+    const double mu = fmax(fabs(st[(3 + c) * kTileTP]), 1e-3);
     need = fmax(need, var / (rel * rel * mu * mu));
   }
-  const int left = ta->budget - r.n;
-  const double want = (need - (double)r.n) * (ta->margin + ta->margin_step * (double)phase + ta->starve_gain * (double)idle);
+  const int left = ta->budget - n;
+  const double want = (need - (double)n) * (ta->margin + ta->margin_step * (double)phase + ta->starve_gain * (double)idle);
   int k = (want < (double)left) ? (int)ceil(want) : left;  // NaN / inf: the whole budget
   k = max(k, min(ta->kinc, left));
   return (uint32_t)min(k, left);
@@ -669,10 +671,10 @@ __device__ __forceinline__ void tile_record(TileLds* tl, const TileArgs* ta, int
       int nn = px.samples[p];
       bool conv = false;
       const int n0 = nn;
+      for (int c = 0; c < 3; c++)
+        st[c * kTileTP] = px.sum[c * np + p], st[(3 + c) * kTileTP] = px.mean[c * np + p],
+        st[(6 + c) * kTileTP] = px.m2[c * np + p];
       if (K > 0) {
-        for (int c = 0; c < 3; c++)
-          st[c * kTileTP] = px.sum[c * np + p], st[(3 + c) * kTileTP] = px.mean[c * np + p],
-          st[(6 + c) * kTileTP] = px.m2[c * np + p];
         const uint64_t base = tile_slot(ta, j, fb, o0);
         replay_pixel_lds(st, nn, conv, ta->L + 3 * base, (int)K, ta->min_spp, ta->rel);
         if (COUNT) {  // the segments of the samples recorded (the rest are discarded)
@@ -688,10 +690,7 @@ __device__ __forceinline__ void tile_record(TileLds* tl, const TileArgs* ta, int
       }
       live = !conv && nn < ta->budget;
       if (live) {
-        PixRec r;  // (only what the prediction reads)
-        for (int c = 0; c < 3; c++) r.mean[c] = px.mean[c * np + p], r.m2[c] = px.m2[c * np + p];
-        r.n = nn;
-        kt = tile_next_batch(r, ta, d.phase, idle);
+        kt = tile_next_batch(st, nn, ta, d.phase, idle);
       } else {
         d.fin[i] = 1u;
       }
