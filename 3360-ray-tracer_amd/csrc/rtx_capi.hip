@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <numeric>
 #include <string>
 #include <thread>
 #include <vector>
@@ -92,7 +93,16 @@ float round_up(double x) {
 
 }  // namespace
 
-constexpr int kCounterWords = 64 + 8 * 16 + 8;  // statistics, queue counts, slot counter(s), [196] segment buffer (0)
+// Fixed-spp frames traced in one sample group are split into kFrameParts launches over
+// consecutive pixel ranges (render_device_impl, "frame parts"), the last part taking
+// kFrameLastShare of the pixels.
+constexpr int kFrameParts = 2;
+constexpr double kFrameLastShare = 0.25;
+constexpr int kMaxFrameParts = 4;
+// statistics, queue counts, then one slot counter block per frame part (8 region counters 128 B
+// apart, [128 + 4] the segment buffer (0), ...)
+constexpr int kSlotBlockWords = 8 * 16 + 8;
+constexpr int kCounterWords = 64 + kMaxFrameParts * kSlotBlockWords;
 
 // Where a render's output goes once a band of it is final (fixed-spp renders): the
 // accumulate of the last sample group runs in kBands bands of the frame's pixels, and after
@@ -136,6 +146,9 @@ struct AdaptTune {
   int tile_split;        // tiles: predicted samples above this are split into two batches (0: default; huge: never)
 };
 static AdaptTune g_tune{0, 0, 0.0, 0, 0, 0, 0, 0, -1.0, -1, -1.0, 0};
+// Overrides of kFrameParts / kFrameLastShare (rtx_internal_frame_parts; 0: the default)
+static int g_frame_parts = 0;
+static double g_frame_last_share = 0.0;
 struct AdaptWs {
   DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer, [134] TileArgs
   DevBuf segs;                                  // counting renders: each slot's path segments (u16)
@@ -179,6 +192,10 @@ struct rtx_scene {
   // banded output copies (BandSink): a copy stream and its ordering events
   hipStream_t copy_stream = nullptr;
   std::vector<hipEvent_t> band_ev;
+  // frame parts after the first: their stream, and events (setup done, each part's end, the
+  // part stream's work done)
+  hipStream_t part_stream = nullptr;
+  std::vector<hipEvent_t> part_ev;
   AdaptWs aw;  // adaptive phases' workspace
   double slot_mem = -1.0;  // bytes the slot buffers may take (slot_target; -1: not yet queried)
   ~rtx_scene() {
@@ -186,7 +203,9 @@ struct rtx_scene {
     aw.release();
     for (auto e : evpool) (void)hipEventDestroy(e);
     for (auto e : band_ev) (void)hipEventDestroy(e);
+    for (auto e : part_ev) (void)hipEventDestroy(e);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    if (part_stream) (void)hipStreamDestroy(part_stream);
     (void)hipSetDevice(device);
     for (DevBuf* b : {&nodes, &prims, &mats, &texs, &images, &fnodes, &tri_n, &px_sum, &px_mean, &px_m2, &px_samples,
                       &px_conv, &lbuf, &queue[0], &queue[1], &counters, &out_rgb, &out_spp, &rays, &hits, &p3_scratch,
@@ -633,6 +652,23 @@ int64_t subset_pixels(const rtx_camera* cam, const rtx_render_params* p, PixelMa
   }
   m.srows = 1, m.sidx = 0, m.scount = 1;
   return (int64_t)m.w * m.h;
+}
+
+// The pixels of map from its local pixel p0 on (p0 a whole number of its rows: stripes of
+// srows rows, or rows of the rectangle), as a map of their own: PixelMap::xy of local pixel i
+// of the result is xy of p0 + i of map.
+PixelMap sub_map(const PixelMap& m, int64_t p0) {
+  PixelMap r = m;
+  if (m.stripes) {
+    const int64_t r0 = p0 / m.W;  // a multiple of srows
+    r.sidx = m.sidx + (int32_t)(r0 / m.srows) * m.scount;
+    r.h = m.h - (int32_t)r0;
+  } else {
+    const int64_t r0 = p0 / std::max(1, m.w);
+    r.y0 = m.y0 + (int32_t)r0;
+    r.h = m.h - (int32_t)r0;
+  }
+  return r;
 }
 
 template <int STACK, bool FAST>
@@ -1500,6 +1536,35 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   uint64_t hot_launches = 0;
   if (timed) HIPC(hipEventRecord(sc->ev[0], s));
   const int pix_blocks = (int)((npix + kBlock - 1) / kBlock);
+  // frame parts (see the loop): fixed-spp persistent frames of one sample group with a band sink
+  int split_parts = 1;
+  int64_t split_pb[kMaxFrameParts + 1] = {0};
+  int split_bands[kMaxFrameParts] = {0};
+  bool split_done = false;
+  if (banded && !phased && prm->mode != RTX_MODE_WAVEFRONT && K >= budget) {
+    const int parts = std::min(kMaxFrameParts, g_frame_parts > 0 ? g_frame_parts : kFrameParts);
+    const double last = g_frame_last_share > 0 ? g_frame_last_share : kFrameLastShare;
+    // part edges: whole rows of the pixel map's layout and whole bands of the sink
+    const int64_t row = map.stripes ? (int64_t)map.srows * map.W : (int64_t)map.w;
+    const int64_t unit = std::lcm<int64_t>(row, std::max<int64_t>(1, sink->align));
+    const int64_t units = npix / unit;  // (a partial unit at the end joins the last part)
+    if (parts > 1 && units >= parts) {
+      split_parts = parts;
+      for (int q = 1; q < parts; q++) {
+        const double f = (1.0 - last) * q / (parts - 1);
+        split_pb[q] = std::max<int64_t>(split_pb[q - 1] + 1, std::min<int64_t>(units - (parts - q), (int64_t)(f * units + 0.5))) * unit;
+      }
+      split_pb[parts] = npix;
+      for (int q = 0; q < parts; q++)  // bands: the last part's the finest (its copy ends the frame)
+        split_bands[q] = q + 1 < parts ? std::max(1, kBands / 2) : kBands;
+    }
+  }
+  if (split_parts > 1)
+    while (sc->band_ev.size() < (size_t)(kBands * kMaxFrameParts + 1)) {
+      hipEvent_t e = nullptr;
+      HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      sc->band_ev.push_back(e);
+    }
   const int wf_grid = std::max(1, std::min<int>(sc->cus * 16, (int)((nslots + kBlock - 1) / kBlock)));
   if (phased) {
     if ((rc = render_adaptive(sc, L, A, prm, px, budget, s, [&](hipStream_t st) -> int {
@@ -1544,6 +1609,60 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
         HIPC(hipGetLastError());
         hot_launches++;
       }
+    } else if (split_parts > 1) {
+      // Frame parts: part q traces pixels [pb[q], pb[q + 1]) with its own slot counters, the
+      // parts after the first on part_stream, so their workgroups take the CUs an earlier
+      // part's drain frees.  Each part's accumulate (its bands and their copies) follows its own
+      // launch on its own stream and runs in the next part's drain; only the last, smallest
+      // part's accumulate follows the frame's last launch.  Kernel boundaries order every
+      // radiance record before its sum; the results are the one-launch frame's bit for bit.
+      if (!sc->part_stream) HIPC(hipStreamCreateWithFlags(&sc->part_stream, hipStreamNonBlocking));
+      while (sc->part_ev.size() < (size_t)(kMaxFrameParts + 3)) {
+        hipEvent_t e = nullptr;
+        HIPC(hipEventCreate(&e));
+        sc->part_ev.push_back(e);
+      }
+      for (int q = 0; q < split_parts; q++)
+        HIPC(hipMemsetAsync(next_slot + q * kSlotBlockWords, 0, 8 * 16 * sizeof(unsigned long long), s));
+      HIPC(hipEventRecord(sc->part_ev[0], s));  // setup done (and the frame's hot start)
+      HIPC(hipStreamWaitEvent(sc->part_stream, sc->part_ev[0], 0));
+      int band0 = 0;
+      for (int q = 0; q < split_parts; q++) {
+        hipStream_t sq = q == 0 ? s : sc->part_stream;
+        RenderArgs Aq = A;
+        Aq.npix = split_pb[q + 1] - split_pb[q];
+        Aq.L = A.L + 3 * split_pb[q] * (int64_t)Kc;
+        Aq.map = sub_map(map, split_pb[q]);
+        Launch Lq = L;
+        Lq.s = sq;
+        rc = prm->mode == RTX_MODE_MEGAKERNEL ? persist_m<true>(Lq, Aq, next_slot + q * kSlotBlockWords)
+                                              : persist_m<false>(Lq, Aq, next_slot + q * kSlotBlockWords);
+        if (rc) return rc;
+        L.build = Lq.build;
+        HIPC(hipEventRecord(sc->part_ev[1 + q], sq));  // part q's end
+        const AccOut out{d_rgb, d_spp, prm->mode == RTX_MODE_MEGAKERNEL ? 1 : 0, prm->spp};
+        const int64_t align = std::max<int64_t>(1, sink->align);
+        const int64_t u0 = split_pb[q] / align, u1 = (split_pb[q + 1] + align - 1) / align;
+        const int nb = split_bands[q];
+        for (int b = 0; b < nb; b++) {
+          const int64_t q0 = std::min<int64_t>(npix, (u0 + (u1 - u0) * b / nb) * align);
+          const int64_t q1 = std::min<int64_t>(npix, (u0 + (u1 - u0) * (b + 1) / nb) * align);
+          if (q1 <= q0) continue;
+          hipLaunchKernelGGL(k_accumulate_sum, dim3((unsigned)((q1 - q0 + kAccPix - 1) / kAccPix)), dim3(kAccWave), 0,
+                             sq, px, A.L, npix, Kc, q0, q1, 1, out);
+          HIPC(hipGetLastError());
+          HIPC(hipEventRecord(sc->band_ev[band0 + b], sq));
+          HIPC(hipStreamWaitEvent(sc->copy_stream, sc->band_ev[band0 + b], 0));
+          if ((rc = sink->copy(sink->ctx, q0, q1, sc->copy_stream))) return rc;
+        }
+        band0 += nb;
+      }
+      HIPC(hipEventRecord(sc->part_ev[kMaxFrameParts + 2], sc->part_stream));  // the part stream's work done
+      HIPC(hipStreamWaitEvent(s, sc->part_ev[kMaxFrameParts + 2], 0));
+      hot_launches++;
+      split_done = true;
+      resolved = true;
+      continue;
     } else {
       HIPC(hipMemsetAsync(next_slot, 0, 8 * 16 * sizeof(unsigned long long), s));
       if ((rc = hot_begin())) return rc;
@@ -1596,8 +1715,8 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     HIPC(hipEventRecord(sc->ev[1], s));
   }
   if (banded) {  // the caller's stream owns the output again once the band copies are done
-    HIPC(hipEventRecord(sc->band_ev[kBands], sc->copy_stream));
-    HIPC(hipStreamWaitEvent(s, sc->band_ev[kBands], 0));
+    HIPC(hipEventRecord(sc->band_ev.back(), sc->copy_stream));
+    HIPC(hipStreamWaitEvent(s, sc->band_ev.back(), 0));
   }
   if (timed) {
     HIPC(hipEventSynchronize(sc->ev[1]));
@@ -1609,6 +1728,13 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
       float hms = 0;
       HIPC(hipEventElapsedTime(&hms, sc->evpool[e], sc->evpool[e + 1]));
       hot_ms += hms;
+    }
+    // a frame in parts: its hot time is the union of the parts' launches (they overlap), from
+    // the first one's start to the last one's end
+    for (int q = 0; split_done && q < split_parts; q++) {
+      float hms = 0;
+      HIPC(hipEventElapsedTime(&hms, sc->part_ev[0], sc->part_ev[1 + q]));
+      if (q == 0 || hms > hot_ms) hot_ms = hms;
     }
     unsigned long long h[13];
     std::memcpy(h, sc->counters_h.p, sizeof h);
@@ -1966,6 +2092,16 @@ extern "C" int rtx_internal_adapt_tune(int32_t tile_kcap, int32_t tile_kinc, dou
     return fail(RTX_ERR_INVALID, "bad tuning value");
   g_tune = AdaptTune{tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap, tile_first_pass, tile_tp, tile_nt,
                      tile_mstep, tile_tail, tile_starve, tile_split};
+  return RTX_OK;
+}
+
+// Test / tuning hook (not in rtx.h): the frame parts of fixed-spp frames (parts: 1 one launch,
+// up to kMaxFrameParts; last_share: the last part's share of the pixels; 0 restores a default).
+// Results never depend on them.
+extern "C" int rtx_internal_frame_parts(int32_t parts, double last_share) {
+  if (parts < 0 || parts > kMaxFrameParts || !(last_share >= 0.0 && last_share < 1.0))
+    return fail(RTX_ERR_INVALID, "bad frame parts");
+  g_frame_parts = parts, g_frame_last_share = last_share;
   return RTX_OK;
 }
 

@@ -365,6 +365,17 @@ def adapt_tune(tile_kcap=0, tile_kinc=0, tile_margin=0.0, phase_slots=0, phase_k
              tile_mstep, tile_tail, tile_starve, tile_split), "rtx_internal_adapt_tune")
 
 
+def frame_parts(parts=0, last_share=0.0):
+    """Test / tuning hook (rtx_internal_frame_parts, not in rtx.h): fixed-spp frames of one
+    sample group with banded output (render_multi) are traced in `parts` launches over
+    consecutive pixel ranges, the last taking `last_share` of the pixels (1: one launch; 0 / 0.0
+    restore the defaults).  Results never depend on it."""
+    f = lib().rtx_internal_frame_parts
+    f.argtypes = [C.c_int32, C.c_double]
+    f.restype = C.c_int
+    _check(f(parts, last_share), "rtx_internal_frame_parts")
+
+
 def render_multi(scenes, cam, spp, max_depth, seed=1234, adaptive=True, mode="persistent", precision="fast",
                  stripe_rows=8, stripe_index=0, stripe_count=0, out=None, schedule=None, min_spp=16,
                  rel_threshold=float(np.float32(0.05)), samples_per_group=0):

@@ -129,6 +129,9 @@ def main():
     ap.add_argument("--adapt-schedule", default="tiles", choices=["tiles", "phases"],
                     help="adaptive renders after the first pass: tiles in one launch (default) or one launch per "
                          "phase (round 3's schedule; RTX_FLAG_ADAPT_PHASES)")
+    ap.add_argument("--frame-parts", default="",
+                    help="fixed-spp frames in P launches over consecutive pixel ranges, the last with share F "
+                         "of the pixels: P or P:F (rtx.frame_parts; 1 = one launch; default: the library's)")
     ap.add_argument("--adapt-tune", default="",
                     help="tuning of the adaptive schedules (rtx.adapt_tune), e.g. tile_first_pass=1,tile_kcap=64 "
                          "(never changes results, only the work)")
@@ -166,6 +169,9 @@ def main():
 
     import rtx
 
+    if args.frame_parts:
+        fp = args.frame_parts.split(":")
+        rtx.frame_parts(int(fp[0]), float(fp[1]) if len(fp) > 1 else 0.0)
     if args.adapt_tune:
         kv = dict(x.split("=") for x in args.adapt_tune.split(","))
         rtx.adapt_tune(**{k: (float(v) if k in ("tile_margin", "tile_mstep", "tile_starve") else int(v)) for k, v in kv.items()})

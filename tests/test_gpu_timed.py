@@ -362,6 +362,40 @@ def test_render_multi_banded_output_one_device(rtx_mod, scenes):
             assert st["rays_total"] == fst["rays_total"]
 
 
+def test_frame_parts_are_bit_identical(rtx_mod, scenes):
+    """Fixed-spp frames of one sample group are traced in several launches over consecutive
+    pixel ranges (frame parts, the later ones on a second stream, each part's banded accumulate
+    and copies behind its own launch).  Any number of parts and any last share give the
+    one-launch frame bit for bit: every mode's sum, both persistent schedules, one and two
+    scenes (stripes) on the device, a frame height that is no multiple of the stripe height,
+    and counts of parts the frame cannot hold (one launch then)."""
+    import torch
+
+    try:
+        for name, cfg, width, depth in (("final", "c2_final", 76, 50), ("bunny", "c3_bunny", 64, 20)):
+            path, d = scenes(name)
+            cam = rtx_mod.camera(rtx_mod.camera_config(cfg, width=width))
+            npix = cam.image_width * cam.image_height
+            other = rtx_mod.DeviceScene(rtx_mod.HostScene.load(path))
+            for mode, precision, schedule in (("persistent", "fast", "park"), ("persistent", "fast", "plain"),
+                                              ("persistent", "parity", None), ("megakernel", "fast", None)):
+                rtx_mod.frame_parts(1)
+                ref, rsp, rst, _ = rtx_mod.render_multi([d], cam, 4, depth, seed=33, adaptive=False, mode=mode,
+                                                        precision=precision, schedule=schedule)
+                for parts, share in ((2, 0.25), (2, 0.6), (3, 0.1), (4, 0.3), (4, 0.95)):
+                    rtx_mod.frame_parts(parts, share)
+                    for group in ([d], [d, other]):
+                        pinned = torch.full((npix, 3), -1.0, dtype=torch.float64).pin_memory()
+                        out = pinned.numpy()
+                        rgb, sp, st, _ = rtx_mod.render_multi(group, cam, 4, depth, seed=33, adaptive=False, mode=mode,
+                                                              precision=precision, schedule=schedule, out=out)
+                        key = (name, mode, precision, schedule, parts, share, len(group))
+                        assert np.array_equal(out, ref) and np.array_equal(sp, rsp), key
+                        assert st["rays_total"] == rst["rays_total"], key
+    finally:
+        rtx_mod.frame_parts()
+
+
 def test_render_multi_rejects_bad_arguments(rtx_mod, scenes):
     _, d = scenes("final")
     cam = rtx_mod.camera(rtx_mod.camera_config("c2_final", width=16))
