@@ -1550,11 +1550,15 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     const int64_t units = npix / unit;  // (a partial unit at the end joins the last part)
     if (parts > 1 && units >= parts) {
       split_parts = parts;
+      int64_t prev = 0;  // (in units; every part at least one)
       for (int q = 1; q < parts; q++) {
         const double f = (1.0 - last) * q / (parts - 1);
-        split_pb[q] = std::max<int64_t>(split_pb[q - 1] + 1, std::min<int64_t>(units - (parts - q), (int64_t)(f * units + 0.5))) * unit;
+        prev = std::max<int64_t>(prev + 1, std::min<int64_t>(units - (parts - q), (int64_t)(f * units + 0.5)));
+        split_pb[q] = prev * unit;
       }
       split_pb[parts] = npix;
+      for (int q = 0; q < parts; q++)  // (never reached: the host check before any launch)
+        if (!(split_pb[q] < split_pb[q + 1] && split_pb[q + 1] <= npix)) return fail(RTX_ERR_INVALID, "bad frame parts");
       for (int q = 0; q < parts; q++)  // bands: the last part's the finest (its copy ends the frame)
         split_bands[q] = q + 1 < parts ? std::max(1, kBands / 2) : kBands;
     }
