@@ -182,7 +182,7 @@ struct TileArgs {
 // buffer: word = (cursor << 32) | T: its T slots are claimed by adding to the cursor (an add
 // returns T with it, so a claim is consistent even when it races a re-layout); rem counts its
 // paths still running; slot s is sample s0[i] + (s - off[i]) of pixel pix[i], off[i] <= s <
-// off[i + 1].  Only the record (one wave at a time per tile: it claims the front's done bit)
+// off[i + 1].  Only the wave holding the tile's lock (its claim, then one record at a time)
 // lays out batches.
 struct TileBuf {
   unsigned long long word;
@@ -197,7 +197,7 @@ struct TileDesc {
   uint32_t npx, phase;
   uint32_t front;  // the front buffer (0 / 1); the other one holds the back batch
   uint32_t done;   // bit b: buffer b's batch has ended (its last path counted off), not yet recorded
-  uint32_t pad_;
+  uint32_t lock;   // 1: a wave lays out this tile's batches (its claim or a record)
   uint32_t pix[kTileTP];
   uint32_t fin[kTileTP];  // 1: the pixel is finished (converged or out of budget)
 };
@@ -574,7 +574,8 @@ __device__ __forceinline__ uint32_t tile_layout(TileLds* tl, int j, int b, int n
 // the others) and lays out its front and back batches (wave-uniform; the whole wave).  false:
 // no free descriptor, or the claim order is used up (then tl->exhausted is set).
 __device__ __forceinline__ bool tile_claim(TileLds* tl, const TileArgs* ta, unsigned long long* ctr, uint32_t region,
-                                           unsigned long long* tstat = nullptr) {
+                                           int& claimed, unsigned long long* tstat = nullptr) {
+  claimed = -1;  // the descriptor claimed (its lock held: the caller runs tile_unlock)
   int j = -1;
   const int nt = ta->nt;
   if (lane_id() == 0)
@@ -611,6 +612,10 @@ __device__ __forceinline__ bool tile_claim(TileLds* tl, const TileArgs* ta, unsi
     }
     return false;
   }
+  // the lock (released by tile_unlock): a wave still holding it found a stale ready bit
+  // of the descriptor's last tile, and lets go at once
+  if (lane_id() == 0)
+    while (atomicCAS(&d.lock, 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(1);
   const uint32_t first = (uint32_t)tid * (uint32_t)ta->tp, nact = *ta->nact;
   const int n = (int)min<uint32_t>((uint32_t)ta->tp, nact - first);
   const int i = (int)lane_id();
@@ -626,15 +631,17 @@ __device__ __forceinline__ bool tile_claim(TileLds* tl, const TileArgs* ta, unsi
   if (i == 0) d.npx = (uint32_t)n, d.phase = 0, d.front = 0, d.done = 0;
   const uint32_t T = tile_layout(tl, j, 0, n, f, s);
   tile_layout(tl, j, 1, n, min(kt - f, (uint32_t)ta->kcap), s + f);
-  if (i == 0) atomicExch(&d.state, T ? 2u : 0u);  // (an active pixel always has a batch)
+  if (i == 0) atomicExch(&d.state, 2u);  // (an active pixel always has a batch)
+  claimed = j;
   return T != 0;
 }
 // Records the front batch of descriptor j while it has ended: replay it into the pixels'
 // statistics (lane i = pixel i of the tile); the back batch becomes the front, and the samples
 // predicted beyond it are laid out as the new back batch in the buffer just recorded
 // (wave-uniform; the whole wave; one wave per tile at a time: it claims the front's done bit).
+// (the caller holds the tile's lock; true: the tile has ended, its descriptor and lock are free)
 template <bool COUNT>
-__device__ __forceinline__ void tile_record(TileLds* tl, const TileArgs* ta, int j) {
+__device__ __forceinline__ bool tile_record_locked(TileLds* tl, const TileArgs* ta, int j) {
   TileDesc& d = tl->d[j];
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // every lane's radiance store, before its count-off
   const int i = (int)lane_id();
@@ -647,17 +654,19 @@ __device__ __forceinline__ void tile_record(TileLds* tl, const TileArgs* ta, int
     if (!(old & (1u << fb))) break;  // the front batch is still running
     if (__ballot(i < n && d.fin[i] == 0u) == 0) {
       // every pixel is finished: the tile ends once the back batch has no path running
+      const bool end = (old & (1u << bb)) != 0u;
       if (i == 0) {
-        if (old & (1u << bb)) {
+        if (end) {
           atomicAnd(&d.done, ~(1u << bb));
           atomicAnd(&tl->avail, ~(3u << (2 * j)));
+          atomicExch(&d.lock, 0u);
           atomicExch(&d.state, 0u);
         } else {
           atomicOr(&d.done, 1u << fb);  // (empty: the back's record finds it ended)
           d.front = (uint32_t)bb;
         }
       }
-      break;
+      return end;
     }
     const uint32_t idle = *(volatile uint32_t*)&tl->idle;
     const bool exh = *(volatile uint32_t*)&tl->exhausted != 0u;
@@ -707,6 +716,27 @@ __device__ __forceinline__ void tile_record(TileLds* tl, const TileArgs* ta, int
     if (i == 0) d.front = (uint32_t)bb, d.phase = d.phase + 1u;
     tile_layout(tl, j, fb, n, kn, sb + kb);
   }
+  return false;
+}
+// Releases the tile's lock.  A batch that ended meanwhile (its ready bit taken by a wave that
+// found the lock held) is marked ready again, for the next wave at the top of its loop.
+__device__ __forceinline__ void tile_unlock(TileLds* tl, int j) {
+  TileDesc& d = tl->d[j];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane_id() == 0) {
+    atomicExch(&d.lock, 0u);
+    const uint32_t f = *(volatile uint32_t*)&d.front, dn = *(volatile uint32_t*)&d.done;
+    if (dn & (1u << f)) atomicOr(&tl->ready, 1u << j);
+  }
+}
+// Records descriptor j's ended batches unless another wave holds its lock (that wave looks
+// again when it lets go).  (Wave-uniform; the whole wave.)
+template <bool COUNT>
+__device__ __forceinline__ void tile_record(TileLds* tl, const TileArgs* ta, int j) {
+  uint32_t got = 0;
+  if (lane_id() == 0) got = atomicCAS(&tl->d[j].lock, 0u, 1u) == 0u ? 1u : 0u;
+  if (!__builtin_amdgcn_readfirstlane(got)) return;
+  if (!tile_record_locked<COUNT>(tl, ta, j)) tile_unlock(tl, j);
 }
 // The wave's exit test: no tile left to claim, none in flight.
 __device__ __forceinline__ bool tiles_done(const TileLds* tl) {
@@ -853,7 +883,11 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
           }
         }
         if (given < nidle && !__builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&tl->exhausted))
-          tile_claim(tl, ta, next_slot, region, COUNT ? A.counters : nullptr);  // its slots go to the next refill
+        {  // its slots go to the next refill
+          int cj;
+          tile_claim(tl, ta, next_slot, region, cj, COUNT ? A.counters : nullptr);
+          if (cj >= 0) tile_unlock(tl, cj);
+        }
       }
     } else if (idle != 0 && !exhausted && (__popcll(idle) >= kRefill || idle == ~0ull)) {
       const uint64_t nidle = (uint64_t)__popcll(idle);

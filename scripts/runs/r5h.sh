@@ -4,7 +4,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/r5h; mkdir -p $O
-timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_parity.py \
+timeout -k 10 400 python -u -m pytest -x -v --timeout 60 --timeout-method thread tests/test_gpu_parity.py \
   -k "adaptive_schedules or group_size or persistent_schedule_equals" > $O/pytest_parity.log 2>&1 || exit 1
 B="--adaptive --steps 6 --warmup 1 --no-cpu-baseline --no-generic-leg"
 run() {  # tag, extra args
