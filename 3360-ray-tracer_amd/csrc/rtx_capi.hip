@@ -93,10 +93,12 @@ float round_up(double x) {
 
 }  // namespace
 
-// Fixed-spp frames traced in one sample group are split into kFrameParts launches over
-// consecutive pixel ranges (render_device_impl, "frame parts"), the last part taking
-// kFrameLastShare of the pixels.
-constexpr int kFrameParts = 2;
+// Fixed-spp frames traced in one sample group may be split into several launches over
+// consecutive pixel ranges (render_device_impl, "frame parts"; rtx_internal_frame_parts), the
+// last part taking kFrameLastShare of the pixels.  Off by default: each part's launch ends in
+// a drain of its own, and the next part's workgroups do not fill it (C3: one launch 17.01 ms,
+// two parts 17.92-18.43, three 19.30, four 20.03; profiles/r04/ab_frame_parts_r5i_c3.txt).
+constexpr int kFrameParts = 1;
 constexpr double kFrameLastShare = 0.25;
 constexpr int kMaxFrameParts = 4;
 // statistics, queue counts, then one slot counter block per frame part (8 region counters 128 B
@@ -815,11 +817,11 @@ int set_segbuf(unsigned long long* ctr, uint16_t* segs, hipStream_t st) {
 // (wavefront.cc:57-225, always adaptive) with the same per-pixel results, on the caller's
 // stream `s`.  Phase 1 traces min_spp samples of every pixel (one uniform launch) and
 // k_adapt_record replays them and sizes each pixel's next batch.  Then either
-//  * tiles (the default; rtx_kernels.h "tile schedule"): the pixels still sampling are cut into
+//  * tiles (RTX_FLAG_ADAPT_TILES; rtx_kernels.h "tile schedule"): the pixels still sampling are cut into
 //    tiles, ordered per region largest predicted work first (flag, scan, compact, keys, radix
 //    sort: all on the stream, no host round trip), and ONE more persistent launch runs every
 //    further phase of every tile, each tile's record inside the workgroup that traces it; or
-//  * phases (RTX_FLAG_ADAPT_PHASES; round 3's schedule): after each phase, record + next batch
+//  * phases (the default; round 3's schedule): after each phase, record + next batch
 //    sizes (k_adapt_record, k_adapt_floor); before each phase, prefix sum and slot map
 //    (k_adapt_expand); the host reads the next phase's slot count (one pinned word) to launch it
 //    or stop; every phase is a launch of its own with its own drain.
@@ -831,7 +833,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   const int64_t npix = A.npix;
   const int K1 = std::min(std::max(1, prm->min_spp), budget);
   static const bool debug = std::getenv("RTX_DEBUG_ADAPT") != nullptr;  // per-phase slot counts on stderr
-  const bool tiles = !(prm->flags & RTX_FLAG_ADAPT_PHASES);
+  const bool tiles = (prm->flags & RTX_FLAG_ADAPT_TILES) && !(prm->flags & RTX_FLAG_ADAPT_PHASES);
   const int64_t phase_slots = g_tune.phase_slots > 0 ? g_tune.phase_slots : kAdaptPhaseSlots;
   if ((int64_t)npix * K1 > 0xFFFFFFFFll) return fail(RTX_ERR_INVALID, "adaptive render: npix x min_spp above 2^32");
   AdaptWs& w = sc->aw;

@@ -756,11 +756,11 @@ __device__ __forceinline__ bool tiles_done(const TileLds* tl) {
 // primitive, so the bunny's tree holds triangles, the final and mixed scenes' spheres), so
 // the walk's leaf tests are compiled for that kind alone.
 // Which slots the kernel draws: uniform groups (MAP = 0), slot p * K + k is sample s0 + k of
-// pixel p; adaptive phases with a slot map (MAP = 1; RTX_FLAG_ADAPT_PHASES), slot i is sample
+// pixel p; adaptive phases with a slot map (MAP = 1; the default adaptive render), slot i is sample
 // smap[i].y of pixel smap[i].x for i below the phase's slot count, where the slot counters'
 // block holds, after the 8 region counters, the slot count (next_slot[128]) and the slot map's
 // address (next_slot[130]), both written by k_adapt_expand; the adaptive tile schedule (MAP =
-// 2, the default adaptive render after the first pass), slots of the tiles in flight in the
+// 2, RTX_FLAG_ADAPT_TILES, after the first pass), slots of the tiles in flight in the
 // block's LDS descriptors (TileArgs at next_slot[134]).  MAP is a template parameter, not a
 // kernel argument: the fixed-spp kernels run at the SGPR limit, and any extra uniform state
 // there reshuffles their register allocation (a runtime switch cost the bunny's build 3.7 %, r3d).

@@ -19,8 +19,11 @@ RTX_SEAM_TMIN = float(np.float32(0.001))
 MODES = {"wavefront": 0, "persistent": 1, "megakernel": 2}
 PRECISIONS = {"parity": 0, "fast": 1}
 RTX_FLAG_COUNT, RTX_FLAG_PARK, RTX_FLAG_NO_PARK, RTX_FLAG_GENERIC, RTX_FLAG_LEAF_STEP = 1, 2, 4, 8, 16
-# adaptive persistent renders: round 3's one-launch-per-phase schedule instead of the tile schedule
+# adaptive persistent renders: one launch per phase (the default; ADAPT_PHASES names it) or the
+# tile schedule (ADAPT_TILES)
 RTX_FLAG_ADAPT_PHASES = 32
+RTX_FLAG_ADAPT_TILES = 64
+ADAPT_SCHEDULE_FLAGS = {None: 0, "phases": RTX_FLAG_ADAPT_PHASES, "tiles": RTX_FLAG_ADAPT_TILES}
 # "park": the PARK schedule with its default walk (speculative on trees of at most 65536 nodes);
 # "park_step": the PARK schedule with the leaf-step walk on every tree
 SCHEDULE_FLAGS = {None: 0, "auto": 0, "park": RTX_FLAG_PARK, "park_step": RTX_FLAG_PARK | RTX_FLAG_LEAF_STEP,
@@ -294,14 +297,14 @@ class DeviceScene:
 
     def render(self, cam, spp, max_depth, seed=1234, adaptive=True, mode="wavefront", precision="parity",
                tile=None, stripes=None, samples_per_group=0, min_spp=16, rel_threshold=float(np.float32(0.05)),
-               count=False, schedule=None, generic=False, adapt_phases=False):
+               count=False, schedule=None, generic=False, adapt_schedule=None):
         p = RenderParams()
         p.spp, p.max_depth, p.adaptive = spp, max_depth, int(bool(adaptive))
         p.min_spp, p.rel_threshold, p.seed = min_spp, rel_threshold, seed
         p.mode, p.precision = MODES[mode], PRECISIONS[precision]
         p.samples_per_group = samples_per_group
         p.flags = ((1 if count else 0) | SCHEDULE_FLAGS[schedule] | (RTX_FLAG_GENERIC if generic else 0)
-                   | (RTX_FLAG_ADAPT_PHASES if adapt_phases else 0))
+                   | ADAPT_SCHEDULE_FLAGS[adapt_schedule])
         if stripes is not None:
             p.stripe_rows, p.stripe_index, p.stripe_count = stripes
         elif tile is not None:

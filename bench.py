@@ -126,9 +126,9 @@ def main():
     ap.add_argument("--adaptive", action="store_true",
                     help="the reference's default sampling (wavefront.cc:42-43, 62-69, 125-127): per-pixel "
                          "adaptive, at least 16 samples, relative error 0.05f, up to the workload's spp")
-    ap.add_argument("--adapt-schedule", default="tiles", choices=["tiles", "phases"],
-                    help="adaptive renders after the first pass: tiles in one launch (default) or one launch per "
-                         "phase (round 3's schedule; RTX_FLAG_ADAPT_PHASES)")
+    ap.add_argument("--adapt-schedule", default="phases", choices=["tiles", "phases"],
+                    help="adaptive renders: one launch per phase (default) or, after the first pass, tiles in "
+                         "one launch (RTX_FLAG_ADAPT_TILES)")
     ap.add_argument("--frame-parts", default="",
                     help="fixed-spp frames in P launches over consecutive pixel ranges, the last with share F "
                          "of the pixels: P or P:F (rtx.frame_parts; 1 = one launch; default: the library's)")
@@ -183,7 +183,7 @@ def main():
     cam = rtx.camera(rtx.camera_config(preset, width=width))
     W, H = cam.image_width, cam.image_height
     sched_flags = (rtx.SCHEDULE_FLAGS[args.schedule] | (rtx.RTX_FLAG_GENERIC if args.generic else 0)
-                   | (rtx.RTX_FLAG_ADAPT_PHASES if args.adapt_schedule == "phases" else 0))
+                   | rtx.ADAPT_SCHEDULE_FLAGS[args.adapt_schedule])
 
     def params(flags=sched_flags, generic=False, adaptive=None):
         p = rtx.RenderParams()

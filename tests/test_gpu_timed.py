@@ -181,7 +181,7 @@ def test_adaptive_full_budget_small_workspace_matches_oracle(rtx_mod, orc, scene
         rtx_mod.adapt_tune(**knobs)
         rgb, sp, st = d.render(cam, spp, depth, seed=616, adaptive=True, mode="persistent", precision="fast",
                                tile=tile, count=True, min_spp=ADAPTIVE_MIN, rel_threshold=ADAPTIVE_REL,
-                               adapt_phases=phases)
+                               adapt_schedule="phases" if phases else "tiles")
     finally:
         rtx_mod.adapt_tune()
     ref_spp = ref_spp.ravel()
