@@ -101,10 +101,6 @@ float round_up(double x) {
 constexpr int kFrameParts = 1;
 constexpr double kFrameLastShare = 0.25;
 constexpr int kMaxFrameParts = 4;
-// Fixed-spp persistent frames trace their rows most expensive first in every slot region
-// (rtx_kernels.h "row order"); rtx_internal_row_order switches it (A/B, tests).
-constexpr bool kRowOrder = true;
-static int g_row_order = -1;  // -1: kRowOrder
 // statistics, queue counts, then one slot counter block per frame part (8 region counters 128 B
 // apart, [128 + 4] the segment buffer (0), ...)
 constexpr int kSlotBlockWords = 8 * 16 + 8;
@@ -191,7 +187,6 @@ struct rtx_scene {
   // render workspace (grow-only)
   DevBuf px_sum, px_mean, px_m2, px_samples, px_conv, lbuf, queue[2], counters, out_rgb, out_spp, rays, hits;
   DevBuf p3_scratch, p3_body;  // device P3 encoding (rtx_p3.h)
-  DevBuf row_buf;              // row order: probe rays and hits, order, inverse
   HostBuf stage_rgb, stage_spp;  // rtx_render_multi: pinned D2H staging of this device's stripes
   HostBuf counters_h;            // timed renders: pinned copy of the statistics counters (read after the end event)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -216,7 +211,7 @@ struct rtx_scene {
     (void)hipSetDevice(device);
     for (DevBuf* b : {&nodes, &prims, &mats, &texs, &images, &fnodes, &tri_n, &px_sum, &px_mean, &px_m2, &px_samples,
                       &px_conv, &lbuf, &queue[0], &queue[1], &counters, &out_rgb, &out_spp, &rays, &hits, &p3_scratch,
-                      &p3_body, &calib_rgb, &row_buf})
+                      &p3_body, &calib_rgb})
       b->release();
     for (auto& t : texels) t.release();
     stage_rgb.release(), stage_spp.release();
@@ -937,7 +932,6 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   auto launch = [&](int g, const Launch& Lg, const RenderArgs& Ag, uint16_t* segs, int64_t pixels) -> int {
     unsigned long long seg0 = 0;
     HIPC(hipMemsetAsync(ctr, 0, 8 * 16 * sizeof(unsigned long long), s));
-    HIPC(hipMemsetAsync(ctr + 8 * 16 + 7, 0, sizeof(unsigned long long), s));  // (no row order)
     if (debug) {
       HIPC(hipStreamSynchronize(s));
       HIPC(hipMemcpy(&seg0, A.counters, sizeof seg0, hipMemcpyDeviceToHost));
@@ -1544,54 +1538,12 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   uint64_t hot_launches = 0;
   if (timed) HIPC(hipEventRecord(sc->ev[0], s));
   const int pix_blocks = (int)((npix + kBlock - 1) / kBlock);
-  // row order (rtx_kernels.h): fixed-spp persistent frames (one pass over every pixel's slots
-  // per group; the accumulate reads each pixel's run through the inverse order).  The probe
-  // rays, their hits and the sort run on the stream before the first launch; the order's
-  // address goes to word 8 * 16 + 7 of the slot counter block (0: image order).
-  const uint32_t* row_inv = nullptr;
-  int32_t row_len = 1;
-  {
-    const int64_t rl = map.stripes ? (int64_t)map.W : (int64_t)map.w;
-    const int64_t nrows = rl > 0 ? npix / rl : 0;
-    const bool on = g_row_order < 0 ? kRowOrder : g_row_order > 0;
-    if (on && sum_path && !phased && prm->mode != RTX_MODE_WAVEFRONT && nrows >= 2 && nrows <= kRowSortMax &&
-        nrows * rl == npix) {
-      const size_t nprobe = (size_t)nrows * kRowProbes;
-      const size_t b_rays = nprobe * sizeof(rtx_ray), b_hits = nprobe * sizeof(rtx_hit);
-      if ((rc = sc->row_buf.reserve(b_rays + b_hits + 2 * (size_t)nrows * sizeof(uint32_t)))) return rc;
-      char* base = (char*)sc->row_buf.p;
-      rtx_ray* pr = (rtx_ray*)base;
-      rtx_hit* ph = (rtx_hit*)(base + b_rays);
-      uint32_t* order = (uint32_t*)(base + b_rays + b_hits);
-      uint32_t* inv = order + nrows;
-      RenderArgs Ap = A;
-      hipLaunchKernelGGL(k_row_rays, dim3((unsigned)((nprobe + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, Ap, pr,
-                         (int32_t)nrows, (int32_t)rl);
-      HIPC(hipGetLastError());
-      const int st = L.fast ? sc->stack_fast : sc->stack_parity;
-      if (L.fast) rc = st == 32 ? launch_intersect<32, true>(sc, pr, (int64_t)nprobe, ph, (double)0.001f, INFINITY, s)
-                                : launch_intersect<64, true>(sc, pr, (int64_t)nprobe, ph, (double)0.001f, INFINITY, s);
-      else rc = st == 32 ? launch_intersect<32, false>(sc, pr, (int64_t)nprobe, ph, (double)0.001f, INFINITY, s)
-                         : launch_intersect<64, false>(sc, pr, (int64_t)nprobe, ph, (double)0.001f, INFINITY, s);
-      if (rc) return rc;
-      hipLaunchKernelGGL(k_row_order, dim3(1), dim3(kRowOrderThreads), 0, s, (const rtx_hit*)ph, (int32_t)nrows, order,
-                         inv);
-      HIPC(hipGetLastError());
-      for (int q = 0; q < kMaxFrameParts; q++) {  // every part's slot counter block (frame parts: their own rows)
-        uint32_t* w = (uint32_t*)(next_slot + q * kSlotBlockWords + 8 * 16 + 7);
-        const unsigned long long v = (unsigned long long)(uintptr_t)order;
-        HIPC(hipMemsetD32Async((hipDeviceptr_t)w, (int)(uint32_t)v, 1, s));
-        HIPC(hipMemsetD32Async((hipDeviceptr_t)(w + 1), (int)(uint32_t)(v >> 32), 1, s));
-      }
-      row_inv = inv, row_len = (int32_t)rl;
-    }
-  }
   // frame parts (see the loop): fixed-spp persistent frames of one sample group with a band sink
   int split_parts = 1;
   int64_t split_pb[kMaxFrameParts + 1] = {0};
   int split_bands[kMaxFrameParts] = {0};
   bool split_done = false;
-  if (banded && !phased && prm->mode != RTX_MODE_WAVEFRONT && K >= budget && !row_inv) {  // (parts keep image order)
+  if (banded && !phased && prm->mode != RTX_MODE_WAVEFRONT && K >= budget) {
     const int parts = std::min(kMaxFrameParts, g_frame_parts > 0 ? g_frame_parts : kFrameParts);
     const double last = g_frame_last_share > 0 ? g_frame_last_share : kFrameLastShare;
     // part edges: whole rows of the pixel map's layout and whole bands of the sink
@@ -1703,7 +1655,7 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
           const int64_t q1 = std::min<int64_t>(npix, (u0 + (u1 - u0) * (b + 1) / nb) * align);
           if (q1 <= q0) continue;
           hipLaunchKernelGGL(k_accumulate_sum, dim3((unsigned)((q1 - q0 + kAccPix - 1) / kAccPix)), dim3(kAccWave), 0,
-                             sq, px, A.L, npix, Kc, q0, q1, 1, out, row_inv, row_len);
+                             sq, px, A.L, npix, Kc, q0, q1, 1, out);
           HIPC(hipGetLastError());
           HIPC(hipEventRecord(sc->band_ev[band0 + b], sq));
           HIPC(hipStreamWaitEvent(sc->copy_stream, sc->band_ev[band0 + b], 0));
@@ -1744,7 +1696,7 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
         const int64_t q1 = std::min<int64_t>(npix, units * (b + 1) / nb * align);
         if (q1 <= q0) continue;
         hipLaunchKernelGGL(k_accumulate_sum, dim3((unsigned)((q1 - q0 + kAccPix - 1) / kAccPix)), dim3(kAccWave), 0,
-                           s, px, A.L, npix, Kc, q0, q1, s0 == 0 ? 1 : 0, out, row_inv, row_len);
+                           s, px, A.L, npix, Kc, q0, q1, s0 == 0 ? 1 : 0, out);
         HIPC(hipGetLastError());
         if (last && banded) {
           HIPC(hipEventRecord(sc->band_ev[b], s));
@@ -2146,14 +2098,6 @@ extern "C" int rtx_internal_adapt_tune(int32_t tile_kcap, int32_t tile_kinc, dou
     return fail(RTX_ERR_INVALID, "bad tuning value");
   g_tune = AdaptTune{tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap, tile_first_pass, tile_tp, tile_nt,
                      tile_mstep, tile_tail, tile_starve, tile_split};
-  return RTX_OK;
-}
-
-// Test / tuning hook (not in rtx.h): the row order of fixed-spp frames (1 on, 0 off, -1 the
-// default).  Results never depend on it.
-extern "C" int rtx_internal_row_order(int32_t on) {
-  if (on < -1 || on > 1) return fail(RTX_ERR_INVALID, "bad row order switch");
-  g_row_order = on;
   return RTX_OK;
 }
 

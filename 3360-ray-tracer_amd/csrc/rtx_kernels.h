@@ -959,17 +959,9 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
         }
         e = make_uint2(d.pix[lo], B.s0[lo] + (s - B.off[lo]));
       }
-      const uint32_t q = MAP ? e.x : (uint32_t)slot / (uint32_t)Ar.K;
-      const int k = MAP ? 0 : (int)((uint32_t)slot - q * (uint32_t)Ar.K);
-      uint32_t p = q;
-      if (MAP == 0) {  // a row order (fixed-spp frames, RowOrder): local row r is traced in row order[r]'s place
-        const uint32_t* const ro = (const uint32_t*)next_slot[8 * 16 + 7];
-        if (ro) {
-          const uint32_t rl = (uint32_t)(Ar.map.stripes ? Ar.map.W : Ar.map.w), r = q / rl;
-          p = ro[r] * rl + (q - r * rl);
-        }
-      }
+      const uint32_t p = MAP ? e.x : (uint32_t)slot / (uint32_t)Ar.K;
       if (kTiles || !(Ar.conv && Ar.conv[p])) {  // (a tile slot is always traced: its count-off ends the batch)
+        const int k = MAP ? 0 : (int)((uint32_t)slot - p * (uint32_t)Ar.K);
         int x, y;
         Ar.map.xy(p, x, y);
         pix = (uint32_t)(y * Ar.map.W + x), smp = MAP ? e.y : (uint32_t)(Ar.s0 + k);
@@ -1406,28 +1398,15 @@ struct AccOut {
   int resolve;  // -1: keep the running sums in px; 0 / 1: write the resolved pixel
   int spp;
 };
-// rows (row_inv != null): the slots were traced in a row order (RowOrder): pixel p of local row
-// r = p / rowlen has its radiance run at row row_inv[r]'s place.
 __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const double* __restrict__ L, int64_t npix,
                                                              int K, int64_t p_begin, int64_t p_end, int first,
-                                                             AccOut out, const uint32_t* __restrict__ row_inv,
-                                                             int32_t rowlen) {
+                                                             AccOut out) {
   __shared__ double st[kAccPix * kAccPitch];
-  __shared__ int64_t run_at[kAccPix];  // each pixel's radiance run (its first double in L)
   const int t = threadIdx.x;
   const int64_t p0 = p_begin + (int64_t)blockIdx.x * kAccPix;
   const int npx = (int)std::min<int64_t>(kAccPix, p_end - p0);
   const int64_t p = p0 + t;
-  if (t < npx) {
-    int64_t lp = p;
-    if (row_inv) {
-      const int64_t r = p / rowlen;
-      lp = (int64_t)row_inv[r] * rowlen + (p - r * rowlen);
-    }
-    run_at[t] = lp * 3 * (int64_t)K;
-  }
-  __syncthreads();
-  const double* __restrict__ base = L;
+  const double* __restrict__ base = L + p0 * 3 * (int64_t)K;
   double sum[3] = {0, 0, 0};
   if (t < npx && !first)
     for (int c = 0; c < 3; c++) sum[c] = px.sum[c * npix + p];
@@ -1442,7 +1421,7 @@ __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const 
 #pragma unroll
       for (int i = 0; i < NL; i++) {
         const int e = t + kAccWave * i, q = e / PP, j = e - q * PP;
-        if (q < npx) v[i] = *(const double2*)(base + run_at[q] + 3 * k0 + 2 * j);
+        if (q < npx) v[i] = *(const double2*)(base + (int64_t)q * 3 * K + 3 * k0 + 2 * j);
       }
     };
     load(0);
@@ -1470,7 +1449,7 @@ __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const 
 #pragma unroll
       for (int i = 0; i < NL; i++) {
         const int e = t + kAccWave * i, q = e / PP, j = e - q * PP;
-        if (q < npx) v[i] = *(const double2*)(base + run_at[q] + 3 * k0 + 2 * j);
+        if (q < npx) v[i] = *(const double2*)(base + (int64_t)q * 3 * K + 3 * k0 + 2 * j);
       }
 #pragma unroll
       for (int i = 0; i < NL; i++) {
@@ -1481,7 +1460,7 @@ __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const 
       const int run = 3 * kc, total = npx * run;
       for (int e = t; e < total; e += kAccWave) {
         const int q = e / run, j = e - q * run;
-        st[q * kAccPitch + j] = base[run_at[q] + 3 * k0 + j];
+        st[q * kAccPitch + j] = base[(int64_t)q * 3 * K + 3 * k0 + j];
       }
     }
     __syncthreads();
@@ -1500,76 +1479,6 @@ __global__ __launch_bounds__(kAccWave) void k_accumulate_sum(PixelSoA px, const 
       for (int c = 0; c < 3; c++) out.rgb[3 * p + c] = sc * sum[c];
       if (out.spp_out) out.spp_out[p] = out.resolve == 1 ? out.spp : n;
     }
-  }
-}
-#endif
-
-// ---------------------------------------------------------------------------------------
-// Row order of fixed-spp frames (RowOrder, render_device_impl).  A persistent launch ends in a
-// drain: paths started just before its slot counters run dry walk on in nearly empty waves
-// (§3).  Sky rows are cheap (one segment per path), rows on geometry are not, so the frame's
-// rows are traced most expensive first, cheapest last, in each of the 8 slot regions: the
-// paths still running when the counters empty are short.  The cost of a row is the number of
-// kRowProbes primary rays across it (sample 0's, no bounces) that hit the scene; rows are
-// sorted by it (most hits first, then image order) and dealt round robin to the 8 regions.
-// Which lane traces a sample changes, not what it computes: the pixels are bit-identical.
-// ---------------------------------------------------------------------------------------
-constexpr int kRowProbes = 64;
-constexpr int kRowSortMax = 8192;  // rows sorted in one workgroup's LDS (larger frames keep image order)
-#ifndef RTX_PERSISTENT_ONLY
-__global__ __launch_bounds__(kBlock) void k_row_rays(RenderArgs A, rtx_ray* __restrict__ rays, int32_t nrows,
-                                                     int32_t rowlen) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= (int64_t)nrows * kRowProbes) return;
-  const int r = (int)(i / kRowProbes), j = (int)(i - (int64_t)r * kRowProbes);
-  const int x0 = (int)(((int64_t)(2 * j + 1) * rowlen) / (2 * kRowProbes));
-  int x, y;
-  A.map.xy((uint32_t)((int64_t)r * rowlen + x0), x, y);
-  Rng g = make_rng(A.seed, (uint32_t)(y * A.map.W + x), 0u, 0u);
-  V3 o, d;
-  get_ray<false>(A.cam, x, y, g, o, d);
-  rtx_ray& out = rays[i];
-  out.origin[0] = o.x, out.origin[1] = o.y, out.origin[2] = o.z;
-  out.direction[0] = d.x, out.direction[1] = d.y, out.direction[2] = d.z;
-}
-// One workgroup: each row's probe hits, a bitonic sort of (kRowProbes - hits, row) in LDS, then
-// sorted row s goes to region s % 8, place s / 8 (regions laid out one after the other):
-// order[place] = row, inv[row] = place.
-constexpr int kRowOrderThreads = 1024;
-__global__ __launch_bounds__(kRowOrderThreads) void k_row_order(const rtx_hit* __restrict__ hits, int32_t nrows,
-                                                                uint32_t* __restrict__ order, uint32_t* __restrict__ inv) {
-  __shared__ uint32_t key[kRowSortMax];
-  int n2 = 1;
-  while (n2 < nrows) n2 <<= 1;
-  for (int r = threadIdx.x; r < n2; r += kRowOrderThreads) {
-    uint32_t k = 0xFFFFFFFFu;
-    if (r < nrows) {
-      int h = 0;
-      for (int j = 0; j < kRowProbes; j++) h += hits[(int64_t)r * kRowProbes + j].hit ? 1 : 0;
-      k = ((uint32_t)(kRowProbes - h) << 20) | (uint32_t)r;  // (nrows <= kRowSortMax < 2^20)
-    }
-    key[r] = k;
-  }
-  __syncthreads();
-  for (int size = 2; size <= n2; size <<= 1)
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = threadIdx.x; i < n2; i += kRowOrderThreads) {
-        const int jx = i ^ stride;
-        if (jx > i) {
-          const bool up = (i & size) == 0;
-          const uint32_t a = key[i], b = key[jx];
-          if ((a > b) == up) key[i] = b, key[jx] = a;
-        }
-      }
-      __syncthreads();
-    }
-  for (int sidx = threadIdx.x; sidx < nrows; sidx += kRowOrderThreads) {
-    const int g = sidx & 7, pos = sidx >> 3;
-    int start = 0;
-    for (int h = 0; h < g; h++) start += (nrows - h + 7) >> 3;
-    const uint32_t row = key[sidx] & 0xFFFFFu;
-    order[start + pos] = row;
-    inv[row] = (uint32_t)(start + pos);
   }
 }
 #endif

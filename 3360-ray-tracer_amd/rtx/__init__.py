@@ -368,16 +368,6 @@ def adapt_tune(tile_kcap=0, tile_kinc=0, tile_margin=0.0, phase_slots=0, phase_k
              tile_mstep, tile_tail, tile_starve, tile_split), "rtx_internal_adapt_tune")
 
 
-def row_order(on=-1):
-    """Test / tuning hook (rtx_internal_row_order, not in rtx.h): fixed-spp persistent frames
-    trace their rows most expensive first in every slot region (1), in image order (0), or the
-    library default (-1).  Results never depend on it."""
-    f = lib().rtx_internal_row_order
-    f.argtypes = [C.c_int32]
-    f.restype = C.c_int
-    _check(f(on), "rtx_internal_row_order")
-
-
 def frame_parts(parts=0, last_share=0.0):
     """Test / tuning hook (rtx_internal_frame_parts, not in rtx.h): fixed-spp frames of one
     sample group with banded output (render_multi) are traced in `parts` launches over

@@ -129,9 +129,6 @@ def main():
     ap.add_argument("--adapt-schedule", default="phases", choices=["tiles", "phases"],
                     help="adaptive renders: one launch per phase (default) or, after the first pass, tiles in "
                          "one launch (RTX_FLAG_ADAPT_TILES)")
-    ap.add_argument("--row-order", type=int, default=-1, choices=[-1, 0, 1],
-                    help="fixed-spp frames: rows most expensive first in each slot region (1), image order (0), "
-                         "the library default (-1; rtx.row_order)")
     ap.add_argument("--frame-parts", default="",
                     help="fixed-spp frames in P launches over consecutive pixel ranges, the last with share F "
                          "of the pixels: P or P:F (rtx.frame_parts; 1 = one launch; default: the library's)")
@@ -172,8 +169,6 @@ def main():
 
     import rtx
 
-    if args.row_order >= 0:
-        rtx.row_order(args.row_order)
     if args.frame_parts:
         fp = args.frame_parts.split(":")
         rtx.frame_parts(int(fp[0]), float(fp[1]) if len(fp) > 1 else 0.0)

@@ -362,43 +362,6 @@ def test_render_multi_banded_output_one_device(rtx_mod, scenes):
             assert st["rays_total"] == fst["rays_total"]
 
 
-def test_row_order_is_bit_identical(rtx_mod, scenes):
-    """Fixed-spp persistent frames trace their rows most expensive first in each slot region
-    (the default; the accumulate reads each pixel's radiance run through the inverse order).
-    Against image order: the same pixels, sample counts and segments, bit for bit, for every
-    mode's sum, both persistent schedules, one and several sample groups, a tile, and the
-    stripes of one and two scenes on the device (render_multi)."""
-    try:
-        for name, cfg, width, depth in (("final", "c2_final", 90, 50), ("bunny", "c3_bunny", 72, 20),
-                                        ("mixed", "c5_mixed", 64, 50)):
-            path, d = scenes(name)
-            cam = rtx_mod.camera(rtx_mod.camera_config(cfg, width=width))
-            other = rtx_mod.DeviceScene(rtx_mod.HostScene.load(path))
-            for mode, precision, schedule in (("persistent", "fast", "park"), ("persistent", "fast", "plain"),
-                                              ("persistent", "parity", None), ("megakernel", "fast", None)):
-                for group in (0, 3):
-                    for tile in (None, (5, 7, 40, 19)):
-                        kw = dict(seed=44, adaptive=False, mode=mode, precision=precision, schedule=schedule,
-                                  samples_per_group=group, tile=tile)
-                        rtx_mod.row_order(0)
-                        ref, rsp, rst = d.render(cam, 5, depth, count=True, **kw)
-                        rtx_mod.row_order(1)
-                        got, gsp, gst = d.render(cam, 5, depth, count=True, **kw)
-                        key = (name, mode, precision, schedule, group, tile)
-                        assert np.array_equal(got, ref) and np.array_equal(gsp, rsp), key
-                        assert gst["rays_total"] == rst["rays_total"], key
-                rtx_mod.row_order(0)
-                ref, rsp, rst, _ = rtx_mod.render_multi([d], cam, 5, depth, seed=45, adaptive=False, mode=mode,
-                                                        precision=precision, schedule=schedule)
-                rtx_mod.row_order(1)
-                for group in ([d], [d, other]):
-                    got, gsp, gst, _ = rtx_mod.render_multi(group, cam, 5, depth, seed=45, adaptive=False, mode=mode,
-                                                            precision=precision, schedule=schedule)
-                    assert np.array_equal(got, ref) and np.array_equal(gsp, rsp), (name, mode, len(group))
-    finally:
-        rtx_mod.row_order()
-
-
 def test_frame_parts_are_bit_identical(rtx_mod, scenes):
     """Fixed-spp frames of one sample group are traced in several launches over consecutive
     pixel ranges (frame parts, the later ones on a second stream, each part's banded accumulate
@@ -409,7 +372,6 @@ def test_frame_parts_are_bit_identical(rtx_mod, scenes):
     import torch
 
     try:
-        rtx_mod.row_order(0)  # (frames in parts keep image order)
         for name, cfg, width, depth in (("final", "c2_final", 76, 50), ("bunny", "c3_bunny", 64, 20)):
             path, d = scenes(name)
             cam = rtx_mod.camera(rtx_mod.camera_config(cfg, width=width))
@@ -432,7 +394,6 @@ def test_frame_parts_are_bit_identical(rtx_mod, scenes):
                         assert st["rays_total"] == rst["rays_total"], key
     finally:
         rtx_mod.frame_parts()
-        rtx_mod.row_order()
 
 
 def test_render_multi_rejects_bad_arguments(rtx_mod, scenes):
