@@ -930,7 +930,8 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
                        budget, kcap, phase_slots, (const unsigned long long*)ap.next_active);
     HIPC(hipGetLastError());
     HIPC(rtxscan::exclusive_scan_u32(ap.knext, w.off.as<uint32_t>(), npix, w.scan_tmp.p, w.scan_tmp.n, s));
-    hipLaunchKernelGGL(k_adapt_expand, dim3(qb), dim3(kBlock), 0, s, (const uint32_t*)ap.knext,
+    hipLaunchKernelGGL(k_adapt_expand, dim3((unsigned)((npix + kExpandPix - 1) / kExpandPix)), dim3(kBlock), 0, s,
+                       (const uint32_t*)ap.knext,
                        (const uint32_t*)w.off.as<uint32_t>(), npix, 1, 0, (const int32_t*)px.samples,
                        w.smap.as<uint2>(), ctr + 8 * 16);
     HIPC(hipGetLastError());

@@ -1280,20 +1280,22 @@ __global__ __launch_bounds__(kBlock) void k_adapt_floor(uint32_t* __restrict__ k
   knext[q] = (uint32_t)min(kn, min(left, kcap));
 }
 // The next phase's slot map: sub-pixel q's batch occupies slots [off[q], off[q] + knext[q]),
-// slot off[q] + k being sample samples[p] + k of pixel p.  One block per 256 sub-pixels; its
-// slots are a contiguous range written by all its threads (coalesced), each finding its
+// slot off[q] + k being sample samples[p] + k of pixel p.  One block per kExpandPix sub-pixels;
+// its slots are a contiguous range written by all its threads (coalesced), each finding its
 // sub-pixel by a search of the block's offsets in LDS.  The last sub-pixel's thread writes the
-// phase's slot count.
+// phase's slot count.  (Few pixels per block: the pixels still sampling cluster, and a block
+// over 256 of them had up to 256 x kcap slots to write while most blocks had none.)
+constexpr int kExpandPix = 32;
 __global__ __launch_bounds__(kBlock) void k_adapt_expand(const uint32_t* __restrict__ knext,
                                                          const uint32_t* __restrict__ off, int64_t nq, int32_t sub_n,
                                                          int32_t sub_j, const int32_t* __restrict__ samples,
                                                          uint2* __restrict__ smap,
                                                          unsigned long long* __restrict__ total) {
-  __shared__ uint32_t s_off[kBlock], s_p[kBlock], s_s0[kBlock];
+  __shared__ uint32_t s_off[kExpandPix], s_p[kExpandPix], s_s0[kExpandPix];
   __shared__ uint32_t s_end;
   const int t = threadIdx.x;
-  const int64_t q0 = (int64_t)blockIdx.x * kBlock, q = q0 + t;
-  const int nb = (int)min<int64_t>(kBlock, nq - q0);
+  const int64_t q0 = (int64_t)blockIdx.x * kExpandPix, q = q0 + t;
+  const int nb = (int)min<int64_t>(kExpandPix, nq - q0);
   bool act = false;
   if (t < nb) {
     const uint32_t k = knext[q], o = off[q];
