@@ -939,6 +939,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
       HIPC(hipEventRecord(sc->ev[2], s));
     }
     int rc2;
+    if (debug) HIPC(hipMemsetAsync(A.counters + 13, 0, 5 * sizeof(unsigned long long), s));  // (the timeline)
     if ((rc2 = mark(s))) return rc2;
     if (L.count && Lg.map != 2 && (rc2 = set_segbuf(ctr, segs, s))) return rc2;
     if ((rc2 = persist_m<false>(Lg, Ag, ctr))) return rc2;
@@ -955,14 +956,14 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
         uint32_t tc[9] = {};
         HIPC(hipMemcpy(tc, w.tcount.p, sizeof tc, hipMemcpyDeviceToHost));
         pixels = tc[8];
-        unsigned long long tt[18] = {};
-        HIPC(hipMemcpy(tt, A.counters, sizeof tt, hipMemcpyDeviceToHost));
-        if (tt[13]) {  // counting build: the tile launch's timeline (us from the first block's start)
-          const double t0 = (double)~tt[13];
-          auto us = [&](unsigned long long v) { return ((double)v - t0) / 100.0; };
-          fprintf(stderr, "rtx adaptive: tiles timeline: claim order used up %.1f .. %.1f us, waves end %.1f .. %.1f us\n",
-                  us(~tt[15]), us(tt[14]), us(~tt[17]), us(tt[16]));
-        }
+      }
+      unsigned long long tt[18] = {};
+      HIPC(hipMemcpy(tt, A.counters, sizeof tt, hipMemcpyDeviceToHost));
+      if (tt[13]) {  // counting build: the launch's timeline (us from the first block's start)
+        const double t0 = (double)~tt[13];
+        auto us = [&](unsigned long long v) { return ((double)v - t0) / 100.0; };
+        fprintf(stderr, "rtx adaptive: %s %d timeline: slots used up %.1f .. %.1f us, waves end %.1f .. %.1f us\n",
+                Lg.map == 2 ? "tiles after phase" : "phase", g, us(~tt[15]), us(tt[14]), us(~tt[17]), us(tt[16]));
       }
       fprintf(stderr, "rtx adaptive: %s %d: %lld pixels, launch %.3f ms, %llu segments (%.0f Mseg/s)\n",
               Lg.map == 2 ? "tiles after phase" : "phase", g, (long long)pixels, ms, seg1 - seg0,
@@ -1717,8 +1718,8 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     HIPC(hipGetLastError());
   }
   if (timed) {  // the statistics come back with the frame: one wait on the end event, no blocking copy after it
-    if ((rc = sc->counters_h.reserve(13 * sizeof(unsigned long long)))) return rc;
-    HIPC(hipMemcpyAsync(sc->counters_h.p, cnt, 13 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    if ((rc = sc->counters_h.reserve(18 * sizeof(unsigned long long)))) return rc;
+    HIPC(hipMemcpyAsync(sc->counters_h.p, cnt, 18 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     HIPC(hipEventRecord(sc->ev[1], s));
   }
   if (banded) {  // the caller's stream owns the output again once the band copies are done
@@ -1743,8 +1744,15 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
       HIPC(hipEventElapsedTime(&hms, sc->part_ev[0], sc->part_ev[1 + q]));
       if (q == 0 || hms > hot_ms) hot_ms = hms;
     }
-    unsigned long long h[13];
+    unsigned long long h[18];
     std::memcpy(h, sc->counters_h.p, sizeof h);
+    static const bool drain_debug = std::getenv("RTX_DEBUG_DRAIN") != nullptr;
+    if (drain_debug && h[13] && !phased) {  // counting builds: the (last) launch's timeline
+      const double t0 = (double)~h[13];
+      auto us = [&](unsigned long long v) { return ((double)v - t0) / 100.0; };
+      fprintf(stderr, "rtx frame timeline: slots used up %.1f .. %.1f us, waves end %.1f .. %.1f us (%lld segments)\n",
+              us(~h[15]), us(h[14]), us(~h[17]), us(h[16]), (long long)h[0]);
+    }
     stats->wave_rounds = h[10];
     stats->wave_rounds_idle = h[11];
     stats->wave_lanes_live = h[12];

@@ -777,13 +777,13 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   TileLds* const tl = (TileLds*)(ldsb + lay.tiles);  // (kTiles)
   const TileArgs* const ta = kTiles ? (const TileArgs*)next_slot[8 * 16 + 6] : nullptr;
   (void)tl, (void)ta;
+  // counting builds: the launch's timeline (wall clock, 100 MHz): [13] ~first block start,
+  // [14] last wave to find the slots (tiles: the claim order) used up, [15] ~first one, [16]
+  // last wave end, [17] ~first wave end
+  if (COUNT && threadIdx.x == 0) atomicMax(&A.counters[13], ~(unsigned long long)wall_clock64());
   if (kTiles) {
     if (blockIdx.x >= (uint32_t)ta->max_blocks) return;  // (the host sizes the grid within it)
     for (uint32_t w = threadIdx.x; w < sizeof(TileLds) / 4; w += kBlock) ((uint32_t*)tl)[w] = 0u;
-    // counting builds: the launch's timeline (wall clock, 100 MHz): [13] ~first block start,
-    // [14] last block to find the claim order used up, [15] ~first one, [16] last wave end,
-    // [17] ~first wave end
-    if (COUNT && threadIdx.x == 0) atomicMax(&A.counters[13], ~(unsigned long long)wall_clock64());
     __syncthreads();
   }
   uint32_t* stk = (uint32_t*)(ldsb + lay.stack) + threadIdx.x;
@@ -919,6 +919,11 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
           chunk_base = nb + used, chunk_left = (ne - nb) - used;
         } else {
           chunk_left = 0, exhausted = true;
+          if (COUNT && lane_id() == 0) {
+            const unsigned long long t = (unsigned long long)wall_clock64();
+            atomicMax(&A.counters[14], t);
+            atomicMax(&A.counters[15], ~t);
+          }
         }
       }
       if (cand < nslots) slot = (uint32_t)cand, fresh = true;
@@ -1093,7 +1098,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
     }
   }
   flush_counters(A, c, segs, prims, COUNT);
-  if (COUNT && kTiles && lane_id() == 0) {
+  if (COUNT && lane_id() == 0) {
     const unsigned long long t = (unsigned long long)wall_clock64();
     atomicMax(&A.counters[16], t);
     atomicMax(&A.counters[17], ~t);
