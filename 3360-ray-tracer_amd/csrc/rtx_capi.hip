@@ -146,8 +146,10 @@ struct AdaptTune {
   int tile_tail;         // tiles: pixels left that take the rest of their budget (< 0: default)
   double tile_starve;    // tiles: margin growth per idle wave of the block at a record (< 0: default)
   int tile_split;        // tiles: predicted samples above this are split into two batches (0: default; huge: never)
+  int first_map;         // the uniform first pass: 1 the phase kernel (block-shared chunks), 0 the uniform-group one (< 0: default)
 };
-static AdaptTune g_tune{0, 0, 0.0, 0, 0, 0, 0, 0, -1.0, -1, -1.0, 0};
+static AdaptTune g_tune{0, 0, 0.0, 0, 0, 0, 0, 0, -1.0, -1, -1.0, 0, -1};
+constexpr int kFirstPassMap = 1;  // the adaptive first pass runs the phase kernel (MAP 1, no slot map)
 // Overrides of kFrameParts / kFrameLastShare (rtx_internal_frame_parts; 0: the default)
 static int g_frame_parts = 0;
 static double g_frame_last_share = 0.0;
@@ -718,7 +720,7 @@ template <int STACK, bool FAST, bool COUNT, bool SCATTER, int PARK, int TK, bool
           int MAP>
 int run_persistent_k1(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
   if (A.stack_slots < 1 || A.stack_slots > STACK + 1) return fail(RTX_ERR_INVALID, "bad traversal stack size");
-  const size_t lds = persist_lds(A.stack_slots, spec_walk(PARK, FAST, SCATTER), MAP == 2).end;
+  const size_t lds = persist_lds(A.stack_slots, spec_walk(PARK, FAST, SCATTER), MAP).end;
   int grid = persistent_grid(
       L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF, MAP>, lds);
   if (L.max_grid > 0) grid = std::min(grid, L.max_grid);
@@ -804,6 +806,13 @@ int persist_m(const Launch& L, const RenderArgs& A, unsigned long long* ns) {
 
 int time_park_schedule(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm, hipStream_t s);
 
+// One 64-bit word of device memory, written in stream order (two 32-bit memsets: no host staging).
+int set_u64(unsigned long long* p, uint64_t v, hipStream_t st) {
+  uint32_t* w = (uint32_t*)p;
+  HIPC(hipMemsetD32Async((hipDeviceptr_t)w, (int)(uint32_t)v, 1, st));
+  HIPC(hipMemsetD32Async((hipDeviceptr_t)(w + 1), (int)(uint32_t)(v >> 32), 1, st));
+  return RTX_OK;
+}
 // Counting renders: the persistent launch's slot counter block names the buffer its paths'
 // segment counts go to (k_persistent COUNT builds read word 8 * 16 + 4 of it).
 int set_segbuf(unsigned long long* ctr, uint16_t* segs, hipStream_t st) {
@@ -1009,7 +1018,15 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   A1.L = sc->lbuf.as<double>();
   A1.conv = nullptr;
   A1.K = K1, A1.s0 = 0;
-  if ((rc = launch(1, L, A1, sc->segs1.as<uint16_t>(), npix))) return rc;
+  // the phase kernel without a slot map (uniform groups: slot p * K1 + k), for its block-shared
+  // chunks: the first pass ends as the phases do, its last slots traced by whole blocks
+  Launch L1 = L;
+  if ((g_tune.first_map >= 0 ? g_tune.first_map : kFirstPassMap) == 1) {
+    L1.map = 1;
+    HIPC(hipMemsetAsync(ctr + 8 * 16 + 2, 0, sizeof(unsigned long long), s));  // (no slot map)
+    if ((rc = set_u64(ctr + 8 * 16, (uint64_t)npix * (uint64_t)K1, s))) return rc;  // the slot count
+  }
+  if ((rc = launch(1, L1, A1, sc->segs1.as<uint16_t>(), npix))) return rc;
   if ((rc = record(1, sc->lbuf.as<double>(), npix))) return rc;
   RenderArgs Ag = A;
   Ag.L = w.lbuf.as<double>();
@@ -2100,13 +2117,14 @@ extern "C" int rtx_internal_check_sincos(int device, int64_t n, uint64_t seed, i
 // phases do (tests/test_gpu_timed.py runs the full budgets through forced small workspaces).
 extern "C" int rtx_internal_adapt_tune(int32_t tile_kcap, int32_t tile_kinc, double tile_margin, int64_t phase_slots,
                                        int32_t phase_kcap, int32_t tile_first_pass, int32_t tile_tp, int32_t tile_nt,
-                                       double tile_mstep, int32_t tile_tail, double tile_starve, int32_t tile_split) {
+                                       double tile_mstep, int32_t tile_tail, double tile_starve, int32_t tile_split,
+                                       int32_t first_map) {
   if (tile_kcap < 0 || tile_kinc < 0 || !(tile_margin >= 0) || phase_slots < 0 || phase_kcap < 0 ||
       tile_first_pass < 0 || tile_first_pass > 2 || tile_tp < 0 || tile_tp > kTileTP || tile_nt < 0 ||
-      tile_nt > kTileNT || tile_split < 0)
+      tile_nt > kTileNT || tile_split < 0 || first_map > 1)
     return fail(RTX_ERR_INVALID, "bad tuning value");
   g_tune = AdaptTune{tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap, tile_first_pass, tile_tp, tile_nt,
-                     tile_mstep, tile_tail, tile_starve, tile_split};
+                     tile_mstep, tile_tail, tile_starve, tile_split, first_map};
   return RTX_OK;
 }
 
@@ -2122,20 +2140,21 @@ extern "C" int rtx_internal_frame_parts(int32_t parts, double last_share) {
 
 // Test hook (not in rtx.h): the persistent kernel's LDS layout (persist_lds) for a traversal
 // stack of stack_slots entries per lane and a schedule (park: 0 plain, 1 PARK with the
-// leaf-step walk, 2 PARK with the speculative walk; + 4: the adaptive tile schedule's launch):
+// leaf-step walk, 2 PARK with the speculative walk; + 4: the adaptive tile schedule's launch,
+// + 8: an adaptive phase launch, with its block-shared slot chunks):
 // out[0..5] = byte offsets of the stack, throughput, hit point, leaf queue, tile descriptors and
 // the block's LDS size; out[6..9] = the first four regions' bytes per lane (entries x element
-// size; they are lane-interleaved with stride kBlock), out[10] = the tile descriptors' bytes
-// (one block-wide region).  tests/test_capi_exports.py checks that the regions are disjoint and
+// size; they are lane-interleaved with stride kBlock), out[10] = the block-wide region's bytes
+// (tile descriptors or chunk words).  tests/test_capi_exports.py checks that the regions are disjoint and
 // inside the block's LDS for every stack size the host can choose.
 extern "C" int rtx_internal_lds_layout(int stack_slots, int park, uint32_t* out) {
-  const bool tiles = (park & 4) != 0;
+  const int block_kind = (park & 4) ? 2 : (park & 8) ? 1 : 0;
   park &= 3;
   if (stack_slots < 1 || stack_slots > 65 || park < 0 || park > 2 || !out) return fail(RTX_ERR_INVALID, "bad argument");
   const bool spec = spec_walk(park, true, false);
-  const PersistLds l = persist_lds(stack_slots, spec, tiles);
+  const PersistLds l = persist_lds(stack_slots, spec, block_kind);
   const uint32_t v[11] = {l.stack, l.thr, l.hitp, l.leafq, l.tiles, l.end, (uint32_t)stack_slots * (spec ? 2u : 4u),
-                          24u, 24u, spec ? kLeafQueue * 4u : 0u, tiles ? (uint32_t)sizeof(TileLds) : 0u};
+                          24u, 24u, spec ? kLeafQueue * 4u : 0u, block_region_bytes(block_kind)};
   std::memcpy(out, v, sizeof v);
   return RTX_OK;
 }

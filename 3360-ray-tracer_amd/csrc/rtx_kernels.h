@@ -221,12 +221,23 @@ static_assert(sizeof(TileBuf) % 8 == 0 && sizeof(TileDesc) % 8 == 0 && sizeof(Ti
 // kSpecMaxNodes nodes, its stack entries being 16-bit)
 constexpr bool spec_walk(int park, bool fast, bool scatter) { return park == 2 && fast && !scatter; }
 constexpr int64_t kSpecMaxNodes = 65536;
-// tiles: the launch runs the tile schedule (MAP == 2), whose descriptors follow the other regions
-constexpr PersistLds persist_lds(int stack_slots, bool spec, bool tiles = false) {
+// The slot chunks of an adaptive phase launch (MAP == 1), one word per wave of the block: a
+// chunk of kChunk slots of one slot region, claimed by LDS adds to its cursor, by its wave and,
+// once the slot counters are dry, by the other waves of the block too.
+// word = region (3 bits) | chunk index in the region (29 bits) | cursor (32 bits)
+struct ChunkLds {
+  unsigned long long w[kBlock / 64];
+};
+// block-wide region after the per-lane ones: 0 none, 1 the chunk words (MAP == 1), 2 the tile
+// schedule's descriptors (MAP == 2)
+constexpr uint32_t block_region_bytes(int kind) {
+  return kind == 2 ? (uint32_t)sizeof(TileLds) : kind == 1 ? (uint32_t)sizeof(ChunkLds) : 0u;
+}
+constexpr PersistLds persist_lds(int stack_slots, bool spec, int block_region = 0) {
   const uint32_t stack_bytes = (uint32_t)stack_slots * kBlock * (spec ? 2u : 4u);
   const uint32_t thr = (stack_bytes + 7u) & ~7u, hitp = thr + 3u * kBlock * 8u, leafq = hitp + 3u * kBlock * 8u;
   const uint32_t tl = leafq + (spec ? (uint32_t)kLeafQueue * kBlock * 4u : 0u);
-  return PersistLds{0u, thr, hitp, leafq, tl, tl + (tiles ? (uint32_t)sizeof(TileLds) : 0u)};
+  return PersistLds{0u, thr, hitp, leafq, tl, tl + block_region_bytes(block_region)};
 }
 
 template <int STACK, bool FAST, bool COUNT, int TK = -1>
@@ -772,7 +783,8 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   // kernels only for fast, non-scatter renders)
   constexpr bool kSpecLds = spec_walk(PARK, FAST, SCATTER);
   constexpr bool kTiles = MAP == 2;
-  const PersistLds lay = persist_lds(A.stack_slots, kSpecLds, kTiles);
+  constexpr bool kShared = MAP == 1;  // block-shared slot chunks (ChunkLds)
+  const PersistLds lay = persist_lds(A.stack_slots, kSpecLds, MAP);
   char* const ldsb = (char*)lds;
   TileLds* const tl = (TileLds*)(ldsb + lay.tiles);  // (kTiles)
   const TileArgs* const ta = kTiles ? (const TileArgs*)next_slot[8 * 16 + 6] : nullptr;
@@ -784,6 +796,12 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   if (kTiles) {
     if (blockIdx.x >= (uint32_t)ta->max_blocks) return;  // (the host sizes the grid within it)
     for (uint32_t w = threadIdx.x; w < sizeof(TileLds) / 4; w += kBlock) ((uint32_t*)tl)[w] = 0u;
+    __syncthreads();
+  }
+  unsigned long long* const cw = (unsigned long long*)(ldsb + lay.tiles);  // (kShared) the chunk words
+  (void)cw;
+  if (kShared) {
+    if (threadIdx.x < kBlock / 64) cw[threadIdx.x] = (unsigned long long)kChunk;  // (no chunk: cursor past any)
     __syncthreads();
   }
   uint32_t* stk = (uint32_t*)(ldsb + lay.stack) + threadIdx.x;
@@ -808,6 +826,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   (void)pseg, (void)segbuf;
   uint64_t chunk_base = 0, chunk_left = 0;  // wave-uniform
   bool exhausted = false;                   // wave-uniform
+  bool dry = false;                         // (kShared) wave-uniform: the slot counters are used up
   uint32_t region = blockIdx.x & 7;         // wave-uniform
   bool has = false;
   Path P;
@@ -889,6 +908,57 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
           if (cj >= 0) tile_unlock(tl, cj);
         }
       }
+    } else if (kShared) {
+      // block-shared chunks: the wave takes slots from its own chunk word (an LDS add), then from
+      // a fresh chunk of the slot counters (installed in its word), and once the counters are
+      // dry from the chunks of the block's other waves, so a block's last slots are traced by
+      // its four waves instead of by the one that happened to claim them
+      if (idle != 0 && !exhausted && (__popcll(idle) >= kRefill || idle == ~0ull)) {
+        const uint32_t nidle = (uint32_t)__popcll(idle);
+        const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane_id()) - 1ull));
+        const int wv = (int)(threadIdx.x >> 6);
+        uint32_t given = 0;
+        auto take = [&](int j) {
+          unsigned long long old = 0;
+          if (lane_id() == 0) old = atomicAdd(&cw[j], (unsigned long long)(nidle - given));
+          old = __shfl(old, 0);
+          const uint32_t r = (uint32_t)(old >> 61), id = (uint32_t)(old >> 32) & 0x1FFFFFFFu, cur = (uint32_t)old;
+          const uint64_t rs = ((uint64_t)r * nslots) >> 3, re = ((uint64_t)(r + 1) * nslots) >> 3;
+          const uint64_t cs = rs + (uint64_t)id * kChunk;
+          const uint32_t csz = cs < re ? (uint32_t)min<uint64_t>(kChunk, re - cs) : 0u;
+          const uint32_t got = cur < csz ? min(nidle - given, csz - cur) : 0u;
+          if (!has && rank >= given && rank < given + got) slot = (uint32_t)(cs + cur + (rank - given)), fresh = true;
+          given += got;
+        };
+        take(wv);
+        if (given < nidle && !dry) {  // a fresh chunk: this wave's region first, then the next ones
+          bool ok = false;
+          for (int tries = 0; tries < 8 && !ok; tries++) {
+            unsigned long long b = 0;
+            if (lane_id() == 0) b = atomicAdd(next_slot + 16 * region, (unsigned long long)kChunk);
+            b = __shfl(b, 0);
+            const uint64_t rs = ((uint64_t)region * nslots) >> 3, re = ((uint64_t)(region + 1) * nslots) >> 3;
+            if (rs + b < re) {
+              ok = true;
+              if (lane_id() == 0)
+                atomicExch(&cw[wv], ((unsigned long long)((region << 29) | (uint32_t)(b / kChunk)) << 32));
+            } else {
+              region = (region + 1) & 7;
+            }
+          }
+          if (ok) take(wv);
+          else dry = true;
+        }
+        for (int m = 1; m < kBlock / 64 && dry && given < nidle; m++) take((wv + m) & (kBlock / 64 - 1));
+        if (dry && given == 0) {  // nothing left anywhere: the counters are dry and so are the block's chunks
+          exhausted = true;
+          if (COUNT && lane_id() == 0) {
+            const unsigned long long t = (unsigned long long)wall_clock64();
+            atomicMax(&A.counters[14], t);
+            atomicMax(&A.counters[15], ~t);
+          }
+        }
+      }
     } else if (idle != 0 && !exhausted && (__popcll(idle) >= kRefill || idle == ~0ull)) {
       const uint64_t nidle = (uint64_t)__popcll(idle);
       const uint64_t rank = (uint64_t)__popcll(idle & ((1ull << lane_id()) - 1ull));
@@ -951,7 +1021,10 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
         __builtin_trap();
       // nslots < 2^32 (checked on the host): 32-bit division
       uint2 e = make_uint2(0u, 0u);
-      if (MAP == 1) e = ((const uint2*)next_slot[8 * 16 + 2])[slot];
+      if (MAP == 1) {  // a phase's slot map, or none: uniform groups (the adaptive first pass)
+        const uint2* const sm = (const uint2*)next_slot[8 * 16 + 2];
+        e = sm ? sm[slot] : make_uint2(slot / (uint32_t)Ar.K, (uint32_t)Ar.s0 + slot % (uint32_t)Ar.K);
+      }
       if (kTiles) {  // slot s of buffer b of descriptor j: the last pixel i with off[i] <= s
         const TileDesc& d = tl->d[slot >> 24];
         const TileBuf& B = d.b[(slot >> 23) & 1u];
