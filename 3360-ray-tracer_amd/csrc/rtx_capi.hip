@@ -952,6 +952,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     if ((rc2 = mark(s))) return rc2;
     if (L.count && Lg.map != 2 && (rc2 = set_segbuf(ctr, segs, s))) return rc2;
     if ((rc2 = persist_m<false>(Lg, Ag, ctr))) return rc2;
+    L.build = Lg.build;  // (the stats report the instantiation launched last)
     if ((rc2 = mark(s))) return rc2;
     hot_launches++;
     if (debug) {
