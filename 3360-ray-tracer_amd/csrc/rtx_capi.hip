@@ -720,7 +720,7 @@ template <int STACK, bool FAST, bool COUNT, bool SCATTER, int PARK, int TK, bool
           int MAP>
 int run_persistent_k1(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
   if (A.stack_slots < 1 || A.stack_slots > STACK + 1) return fail(RTX_ERR_INVALID, "bad traversal stack size");
-  const size_t lds = persist_lds(A.stack_slots, spec_walk(PARK, FAST, SCATTER), MAP).end;
+  const size_t lds = persist_lds(A.stack_slots, spec_walk(PARK, FAST, SCATTER), block_region_kind(MAP, SCATTER)).end;
   int grid = persistent_grid(
       L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF, MAP>, lds);
   if (L.max_grid > 0) grid = std::min(grid, L.max_grid);

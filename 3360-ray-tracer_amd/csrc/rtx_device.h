@@ -28,6 +28,9 @@
 #ifndef RTX_LEAF_STEP
 #define RTX_LEAF_STEP 0  // lean walk: at most one leaf test per lane and loop iteration (trace4_run_step)
 #endif
+#ifndef RTX_SHARED_CHUNKS0
+#define RTX_SHARED_CHUNKS0 0  // uniform-group launches (MAP 0) with the block-shared slot chunks too (A/B)
+#endif
 #ifndef RTX_CAM_KARG
 #define RTX_CAM_KARG 0  // Lambertian texture-free builds: the camera read from the argument segment at refill (A/B)
 #endif

@@ -233,6 +233,10 @@ struct ChunkLds {
 constexpr uint32_t block_region_bytes(int kind) {
   return kind == 2 ? (uint32_t)sizeof(TileLds) : kind == 1 ? (uint32_t)sizeof(ChunkLds) : 0u;
 }
+// which block-wide region a launch of k_persistent<..., SCATTER, ..., MAP> has
+constexpr int block_region_kind(int map, bool scatter) {
+  return map == 2 ? 2 : (map == 1 || (map == 0 && RTX_SHARED_CHUNKS0 && !scatter)) ? 1 : 0;
+}
 constexpr PersistLds persist_lds(int stack_slots, bool spec, int block_region = 0) {
   const uint32_t stack_bytes = (uint32_t)stack_slots * kBlock * (spec ? 2u : 4u);
   const uint32_t thr = (stack_bytes + 7u) & ~7u, hitp = thr + 3u * kBlock * 8u, leafq = hitp + 3u * kBlock * 8u;
@@ -783,8 +787,8 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   // kernels only for fast, non-scatter renders)
   constexpr bool kSpecLds = spec_walk(PARK, FAST, SCATTER);
   constexpr bool kTiles = MAP == 2;
-  constexpr bool kShared = MAP == 1;  // block-shared slot chunks (ChunkLds)
-  const PersistLds lay = persist_lds(A.stack_slots, kSpecLds, MAP);
+  constexpr bool kShared = block_region_kind(MAP, SCATTER) == 1;  // block-shared slot chunks (ChunkLds)
+  const PersistLds lay = persist_lds(A.stack_slots, kSpecLds, block_region_kind(MAP, SCATTER));
   char* const ldsb = (char*)lds;
   TileLds* const tl = (TileLds*)(ldsb + lay.tiles);  // (kTiles)
   const TileArgs* const ta = kTiles ? (const TileArgs*)next_slot[8 * 16 + 6] : nullptr;

@@ -15,3 +15,6 @@ for rep in 1 2; do
     python3 scripts/sweep_summary.py "c3a first_map=$arm rep $rep" $O/c3a_fm${arm}_$rep.json | tee -a $O/ab.txt
   done
 done
+# the uniform-group launch with block-shared chunks (variant build) on fixed-spp C3 / C2
+timeout -k 10 900 bash scripts/ab.sh r5q_shared0_c3 "--no-generic-leg --no-adaptive-leg --no-cpu-baseline" default 3360-ray-tracer_amd/variants/librtx_shared0.so > /dev/null || exit 1
+cat gpurun_out/ab_r5q_shared0_c3.txt
