@@ -28,6 +28,10 @@ constexpr int kRefillMin = 24;      // persistent lanes: refill once this many l
 constexpr int kRefillMinPark = 16;  // the same for the PARK kernel
 constexpr int kParkAt = 16;  // PARK kernel: park traversals once at most this many lanes still walk (ab_parkT_*)
 constexpr int kChunk = 256;  // persistent: slots taken per atomic on a region's slot counter (ab_chunk_*)
+#ifndef RTX_CHUNK_SHARED
+#define RTX_CHUNK_SHARED 256
+#endif
+constexpr int kChunkShared = RTX_CHUNK_SHARED;  // the same for the block-shared chunks (adaptive phase launches)
 
 // Pixel subset of the image handled by one call (rectangle or interleaved row stripes).
 struct PixelMap {
@@ -805,7 +809,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   unsigned long long* const cw = (unsigned long long*)(ldsb + lay.tiles);  // (kShared) the chunk words
   (void)cw;
   if (kShared) {
-    if (threadIdx.x < kBlock / 64) cw[threadIdx.x] = (unsigned long long)kChunk;  // (no chunk: cursor past any)
+    if (threadIdx.x < kBlock / 64) cw[threadIdx.x] = (unsigned long long)kChunkShared;  // (no chunk: cursor past any)
     __syncthreads();
   }
   uint32_t* stk = (uint32_t*)(ldsb + lay.stack) + threadIdx.x;
@@ -928,8 +932,8 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
           old = __shfl(old, 0);
           const uint32_t r = (uint32_t)(old >> 61), id = (uint32_t)(old >> 32) & 0x1FFFFFFFu, cur = (uint32_t)old;
           const uint64_t rs = ((uint64_t)r * nslots) >> 3, re = ((uint64_t)(r + 1) * nslots) >> 3;
-          const uint64_t cs = rs + (uint64_t)id * kChunk;
-          const uint32_t csz = cs < re ? (uint32_t)min<uint64_t>(kChunk, re - cs) : 0u;
+          const uint64_t cs = rs + (uint64_t)id * kChunkShared;
+          const uint32_t csz = cs < re ? (uint32_t)min<uint64_t>(kChunkShared, re - cs) : 0u;
           const uint32_t got = cur < csz ? min(nidle - given, csz - cur) : 0u;
           if (!has && rank >= given && rank < given + got) slot = (uint32_t)(cs + cur + (rank - given)), fresh = true;
           given += got;
@@ -939,13 +943,13 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
           bool ok = false;
           for (int tries = 0; tries < 8 && !ok; tries++) {
             unsigned long long b = 0;
-            if (lane_id() == 0) b = atomicAdd(next_slot + 16 * region, (unsigned long long)kChunk);
+            if (lane_id() == 0) b = atomicAdd(next_slot + 16 * region, (unsigned long long)kChunkShared);
             b = __shfl(b, 0);
             const uint64_t rs = ((uint64_t)region * nslots) >> 3, re = ((uint64_t)(region + 1) * nslots) >> 3;
             if (rs + b < re) {
               ok = true;
               if (lane_id() == 0)
-                atomicExch(&cw[wv], ((unsigned long long)((region << 29) | (uint32_t)(b / kChunk)) << 32));
+                atomicExch(&cw[wv], ((unsigned long long)((region << 29) | (uint32_t)(b / kChunkShared)) << 32));
             } else {
               region = (region + 1) & 7;
             }
