@@ -29,7 +29,7 @@ constexpr int kRefillMinPark = 16;  // the same for the PARK kernel
 constexpr int kParkAt = 16;  // PARK kernel: park traversals once at most this many lanes still walk (ab_parkT_*)
 constexpr int kChunk = 256;  // persistent: slots taken per atomic on a region's slot counter (ab_chunk_*)
 #ifndef RTX_CHUNK_SHARED
-#define RTX_CHUNK_SHARED 256
+#define RTX_CHUNK_SHARED 128
 #endif
 constexpr int kChunkShared = RTX_CHUNK_SHARED;  // the same for the block-shared chunks (adaptive phase launches)
 
