@@ -806,13 +806,6 @@ int persist_m(const Launch& L, const RenderArgs& A, unsigned long long* ns) {
 
 int time_park_schedule(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm, hipStream_t s);
 
-// One 64-bit word of device memory, written in stream order (two 32-bit memsets: no host staging).
-int set_u64(unsigned long long* p, uint64_t v, hipStream_t st) {
-  uint32_t* w = (uint32_t*)p;
-  HIPC(hipMemsetD32Async((hipDeviceptr_t)w, (int)(uint32_t)v, 1, st));
-  HIPC(hipMemsetD32Async((hipDeviceptr_t)(w + 1), (int)(uint32_t)(v >> 32), 1, st));
-  return RTX_OK;
-}
 // Counting renders: the persistent launch's slot counter block names the buffer its paths'
 // segment counts go to (k_persistent COUNT builds read word 8 * 16 + 4 of it).
 int set_segbuf(unsigned long long* ctr, uint16_t* segs, hipStream_t st) {
@@ -921,7 +914,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ap.rec_segs = A.counters + 9;
     ap.active = ctr + 8 * 16 + 1;
     ap.next_active = ctr + 8 * 16 + 3;
-    HIPC(hipMemsetAsync(ap.next_active, 0, sizeof(unsigned long long), s));
+    // (ap.next_active was zeroed with the phase's slot counter block, k_slot_block_init)
     hipLaunchKernelGGL(k_adapt_record, dim3(qb), dim3(kBlock), 0, s, px, Lph, npix, npix, ap);
     HIPC(hipGetLastError());
     if (tiles) return RTX_OK;
@@ -939,9 +932,13 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     return RTX_OK;
   };
   // one persistent launch of a phase; debug: its time and segments on stderr
-  auto launch = [&](int g, const Launch& Lg, const RenderArgs& Ag, uint16_t* segs, int64_t pixels) -> int {
+  // uniform: the launch's slot count (no slot map: uniform groups); 0: the slot map's, from k_adapt_expand
+  auto launch = [&](int g, const Launch& Lg, const RenderArgs& Ag, uint16_t* segs, int64_t pixels,
+                    uint64_t uniform = 0) -> int {
     unsigned long long seg0 = 0;
-    HIPC(hipMemsetAsync(ctr, 0, 8 * 16 * sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_slot_block_init, dim3(1), dim3(8 * 16), 0, s, ctr, uniform ? 1 : 0,
+                       (unsigned long long)uniform, 0ull);
+    HIPC(hipGetLastError());
     if (debug) {
       HIPC(hipStreamSynchronize(s));
       HIPC(hipMemcpy(&seg0, A.counters, sizeof seg0, hipMemcpyDeviceToHost));
@@ -1022,12 +1019,10 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   // the phase kernel without a slot map (uniform groups: slot p * K1 + k), for its block-shared
   // chunks: the first pass ends as the phases do, its last slots traced by whole blocks
   Launch L1 = L;
-  if ((g_tune.first_map >= 0 ? g_tune.first_map : kFirstPassMap) == 1) {
-    L1.map = 1;
-    HIPC(hipMemsetAsync(ctr + 8 * 16 + 2, 0, sizeof(unsigned long long), s));  // (no slot map)
-    if ((rc = set_u64(ctr + 8 * 16, (uint64_t)npix * (uint64_t)K1, s))) return rc;  // the slot count
-  }
-  if ((rc = launch(1, L1, A1, sc->segs1.as<uint16_t>(), npix))) return rc;
+  const bool first_map1 = (g_tune.first_map >= 0 ? g_tune.first_map : kFirstPassMap) == 1;
+  if (first_map1) L1.map = 1;
+  if ((rc = launch(1, L1, A1, sc->segs1.as<uint16_t>(), npix, first_map1 ? (uint64_t)npix * (uint64_t)K1 : 0)))
+    return rc;
   if ((rc = record(1, sc->lbuf.as<double>(), npix))) return rc;
   RenderArgs Ag = A;
   Ag.L = w.lbuf.as<double>();
@@ -1492,14 +1487,14 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   // fixed spp (RecordSample's in-order sum, or the megakernel's DefaultSampler): only the
   // running sum and count matter, and the first group starts them (k_accumulate_sum `first`)
   const bool sum_path = sum_path_of(prm);
-  if (!sum_path) {
-    HIPC(hipMemsetAsync(sc->px_sum.p, 0, npix * 3 * sizeof(double), s));
-    HIPC(hipMemsetAsync(sc->px_mean.p, 0, npix * 3 * sizeof(double), s));
-    HIPC(hipMemsetAsync(sc->px_m2.p, 0, npix * 3 * sizeof(double), s));
-    HIPC(hipMemsetAsync(sc->px_samples.p, 0, npix * sizeof(int32_t), s));
-    HIPC(hipMemsetAsync(sc->px_conv.p, 0, npix, s));
+  {
+    const PixelSoA pz{sc->px_sum.as<double>(), sc->px_mean.as<double>(), sc->px_m2.as<double>(),
+                      sc->px_samples.as<int32_t>(), sc->px_conv.as<uint8_t>()};
+    const int64_t n = std::max<int64_t>(sum_path ? 0 : npix, kCounterWords);
+    hipLaunchKernelGGL(k_frame_init, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, pz, npix,
+                       sum_path ? 0 : 1, sc->counters.as<unsigned long long>(), kCounterWords);
+    HIPC(hipGetLastError());
   }
-  HIPC(hipMemsetAsync(sc->counters.p, 0, kCounterWords * sizeof(unsigned long long), s));
   const bool banded = sum_path && sink && npix > 0;
   if (banded) {
     if (!sc->copy_stream) HIPC(hipStreamCreateWithFlags(&sc->copy_stream, hipStreamNonBlocking));

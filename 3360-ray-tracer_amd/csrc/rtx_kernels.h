@@ -1623,6 +1623,29 @@ __global__ __launch_bounds__(kBlock) void k_accumulate_mk_adaptive(PixelSoA px, 
 // (mega_kernel.h + sampler.h:32,79): pixel /= num_samples (DefaultSampler) or /= samples
 // (AdaptiveSampler).
 #ifndef RTX_PERSISTENT_ONLY  // rtx_park.hip: the persistent kernel's PARK instantiations only
+// A frame's start in one launch instead of one fill per buffer (each fill is a launch with its
+// own gap): the pixel statistics (zero_px) and the statistics counters.
+__global__ __launch_bounds__(kBlock) void k_frame_init(PixelSoA px, int64_t npix, int zero_px,
+                                                       unsigned long long* __restrict__ counters, int nwords) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i < nwords) counters[i] = 0ull;
+  if (!zero_px || i >= npix) return;
+  for (int c = 0; c < 3; c++) px.sum[c * npix + i] = 0.0, px.mean[c * npix + i] = 0.0, px.m2[c * npix + i] = 0.0;
+  px.samples[i] = 0;
+  px.conv[i] = 0;
+}
+// An adaptive launch's slot counter block: the 8 region counters and the next phase's pixel
+// count (word 8 * 16 + 3, k_adapt_record's) zeroed, the slot count and the slot map's address
+// set (set: 0 keeps them, as k_adapt_expand wrote them).
+__global__ void k_slot_block_init(unsigned long long* __restrict__ ctr, int set, unsigned long long nslots,
+                                  unsigned long long smap) {
+  const int i = (int)threadIdx.x;
+  if (i < 8 * 16) ctr[i] = 0ull;
+  if (i == 0) {
+    ctr[8 * 16 + 3] = 0ull;
+    if (set) ctr[8 * 16] = nslots, ctr[8 * 16 + 2] = smap;
+  }
+}
 __global__ __launch_bounds__(kBlock) void k_resolve(PixelSoA px, int64_t npix, int megakernel, int spp,
                                                     double* __restrict__ rgb, int32_t* __restrict__ spp_out) {
   // megakernel: 1 = DefaultSampler (divide by spp), 2 = AdaptiveSampler (by the pixel's count)
