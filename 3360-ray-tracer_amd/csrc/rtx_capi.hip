@@ -1086,13 +1086,11 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     const unsigned long long nsl = ((const volatile unsigned long long*)w.total_h.p)[0];
     const int64_t active = (int64_t)((const volatile unsigned long long*)w.total_h.p)[1];
     if (nsl == 0) break;
-    const bool snap_now = !snapped && active * 8 <= npix;
-    if (snap_now) {  // (record(g - 1) wrote this phase's batches to w.k[g & 1])
+    if (!snapped && active * 8 <= npix) {  // (record(g - 1) wrote this phase's batches to w.k[g & 1])
       snapped = true;
-      if ((rc = snap((const uint32_t*)w.k[g & 1].as<uint32_t>(), active, 0))) return rc;
+      if ((rc = snap((const uint32_t*)w.k[g & 1].as<uint32_t>(), active))) return rc;
     }
     if ((rc = launch(g, Lg, Ag, w.segs.as<uint16_t>(), active))) return rc;
-    if (snap_now && (rc = snap(nullptr, active, 1))) return rc;  // (its copies, the phase queued)
     if ((rc = record(g, Ag.L, active))) return rc;
   }
   return RTX_OK;
@@ -1609,17 +1607,8 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   // the pixels sampling then are listed, and their final output comes back as a patch list
   int64_t patch_n = 0;
   sc->patch_n = 0;
-  // stage 0 (before the phase's launch): resolve, list the pixels still sampling, mark the
-  // output's readiness; stage 1 (the phase queued): the copies, once the output is ready, on the
-  // copy stream with no device-side wait (so they take the DMA engines, not blit kernels that
-  // would wait for CUs the phase's launch holds)
-  auto snap = [&](const uint32_t* knext, int64_t active, int stage) -> int {
+  auto snap = [&](const uint32_t* knext, int64_t active) -> int {
     if (!sink || !sink->early || !g_early_output) return RTX_OK;
-    if (stage == 1) {
-      if (patch_n == 0) return RTX_OK;
-      HIPC(hipEventSynchronize(sc->band_ev[0]));
-      return sink->early(sink->ctx, sc->copy_stream);
-    }
     AdaptWs& w = sc->aw;
     int rc2;
     if ((rc2 = w.patch_flag.reserve(npix * sizeof(uint32_t)))) return rc2;
@@ -1636,6 +1625,8 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
       sc->band_ev.push_back(e);
     }
     HIPC(hipEventRecord(sc->band_ev[0], s));
+    HIPC(hipStreamWaitEvent(sc->copy_stream, sc->band_ev[0], 0));
+    if ((rc2 = sink->early(sink->ctx, sc->copy_stream))) return rc2;
     uint32_t* flag = w.patch_flag.as<uint32_t>();
     uint32_t* pos = w.patch_pos.as<uint32_t>();
     hipLaunchKernelGGL(k_tile_flags, dim3(pix_blocks), dim3(kBlock), 0, s, knext, npix, flag);
