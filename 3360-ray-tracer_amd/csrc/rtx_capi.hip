@@ -156,7 +156,6 @@ static AdaptTune g_tune{0, 0, 0.0, 0, 0, 0, 0, 0, -1.0, -1, -1.0, 0, -1};
 constexpr int kFirstPassMap = 1;  // the adaptive first pass runs the phase kernel (MAP 1, no slot map)
 // Overrides of kFrameParts / kFrameLastShare (rtx_internal_frame_parts; 0: the default)
 static int g_frame_parts = 0;
-static bool g_early_output = true;  // rtx_internal_early_output
 static double g_frame_last_share = 0.0;
 struct AdaptWs {
   DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer, [134] TileArgs
@@ -1608,7 +1607,7 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   int64_t patch_n = 0;
   sc->patch_n = 0;
   auto snap = [&](const uint32_t* knext, int64_t active) -> int {
-    if (!sink || !sink->early || !g_early_output) return RTX_OK;
+    if (!sink || !sink->early) return RTX_OK;
     AdaptWs& w = sc->aw;
     int rc2;
     if ((rc2 = w.patch_flag.reserve(npix * sizeof(uint32_t)))) return rc2;
@@ -2211,15 +2210,6 @@ extern "C" int rtx_internal_adapt_tune(int32_t tile_kcap, int32_t tile_kinc, dou
     return fail(RTX_ERR_INVALID, "bad tuning value");
   g_tune = AdaptTune{tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap, tile_first_pass, tile_tp, tile_nt,
                      tile_mstep, tile_tail, tile_starve, tile_split, first_map};
-  return RTX_OK;
-}
-
-// Test / tuning hook (not in rtx.h): adaptive frames through rtx_render_multi send their output
-// to the host early, during the last phases, with a patch list after (1, the default), or whole
-// at the end (0).  Results never depend on it.
-extern "C" int rtx_internal_early_output(int32_t on) {
-  if (on < 0 || on > 1) return fail(RTX_ERR_INVALID, "bad early output switch");
-  g_early_output = on != 0;
   return RTX_OK;
 }
 

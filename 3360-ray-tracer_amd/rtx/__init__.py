@@ -370,16 +370,6 @@ def adapt_tune(tile_kcap=0, tile_kinc=0, tile_margin=0.0, phase_slots=0, phase_k
              tile_mstep, tile_tail, tile_starve, tile_split, first_map), "rtx_internal_adapt_tune")
 
 
-def early_output(on=True):
-    """Test / tuning hook (rtx_internal_early_output, not in rtx.h): adaptive frames through
-    render_multi send their output to the host during the last phases, with a patch list after
-    (True, the default), or whole at the end (False).  Results never depend on it."""
-    f = lib().rtx_internal_early_output
-    f.argtypes = [C.c_int32]
-    f.restype = C.c_int
-    _check(f(1 if on else 0), "rtx_internal_early_output")
-
-
 def frame_parts(parts=0, last_share=0.0):
     """Test / tuning hook (rtx_internal_frame_parts, not in rtx.h): fixed-spp frames of one
     sample group with banded output (render_multi) are traced in `parts` launches over

@@ -129,8 +129,6 @@ def main():
     ap.add_argument("--adapt-schedule", default="phases", choices=["tiles", "phases"],
                     help="adaptive renders: one launch per phase (default) or, after the first pass, tiles in "
                          "one launch (RTX_FLAG_ADAPT_TILES)")
-    ap.add_argument("--no-early-output", action="store_true",
-                    help="adaptive frames: the output to the host whole at the end (rtx.early_output(False))")
     ap.add_argument("--frame-parts", default="",
                     help="fixed-spp frames in P launches over consecutive pixel ranges, the last with share F "
                          "of the pixels: P or P:F (rtx.frame_parts; 1 = one launch; default: the library's)")
@@ -171,8 +169,6 @@ def main():
 
     import rtx
 
-    if args.no_early_output:
-        rtx.early_output(False)
     if args.frame_parts:
         fp = args.frame_parts.split(":")
         rtx.frame_parts(int(fp[0]), float(fp[1]) if len(fp) > 1 else 0.0)

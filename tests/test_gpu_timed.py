@@ -384,14 +384,8 @@ def test_render_multi_adaptive_early_output(rtx_mod, scenes):
                     out = torch.full((npix, 3), -1.0, dtype=torch.float64).pin_memory().numpy()
                 else:
                     out = np.full((npix, 3), -1.0)
-                for early in (True, False):
-                    out[:] = -1.0
-                    try:
-                        rtx_mod.early_output(early)
-                        rgb, sp, _, _ = rtx_mod.render_multi(group, cam, spp, depth, out=out, **kw)
-                    finally:
-                        rtx_mod.early_output()
-                    assert np.array_equal(out, full) and np.array_equal(sp, fsp), (name, len(group), pinned, early)
+                rgb, sp, _, _ = rtx_mod.render_multi(group, cam, spp, depth, out=out, **kw)
+                assert np.array_equal(out, full) and np.array_equal(sp, fsp), (name, len(group), pinned)
 
 
 def test_frame_parts_are_bit_identical(rtx_mod, scenes):
