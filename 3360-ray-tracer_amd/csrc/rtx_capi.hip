@@ -115,10 +115,6 @@ struct BandSink {
   int64_t align;
   int (*copy)(void* ctx, int64_t p0, int64_t p1, hipStream_t cs);
   void* ctx;
-  // adaptive renders (optional): the whole output (colours and sample counts) to the host on
-  // the copy stream while the last phases still run; the pixels that change after it come back
-  // as a patch list (rtx_scene::patch_h, applied by the caller after its synchronisation)
-  int (*early)(void* ctx, hipStream_t cs) = nullptr;
 };
 constexpr int kBands = 8;  // bands of the last accumulate and of the D2H copies that overlap them (ab_bands_*: 2 / 4 / 8 / 16)
 
@@ -164,11 +160,10 @@ struct AdaptWs {
   // temporary storage, per-region tile counts [0..8) + active pixel count [8], TileArgs
   DevBuf act, tkeys[2], tvals[2], sort_tmp, tcount, targs;
   HostBuf total_h;                              // pinned copy of the next phase's slot count
-  DevBuf patch_flag, patch_pos, patch_idx, patch_val;  // the early output's patch list (render_adaptive snapshot)
   hipEvent_t ev = nullptr;                      // total_h written
   void release() {
     for (DevBuf* b : {&lbuf, &smap, &k[0], &k[1], &off, &scan_tmp, &ctr, &segs, &act, &tkeys[0], &tkeys[1], &tvals[0],
-                      &tvals[1], &sort_tmp, &tcount, &targs, &patch_flag, &patch_pos, &patch_idx, &patch_val})
+                      &tvals[1], &sort_tmp, &tcount, &targs})
       b->release();
     total_h.release();
     if (ev) (void)hipEventDestroy(ev);
@@ -196,8 +191,6 @@ struct rtx_scene {
   DevBuf p3_scratch, p3_body;  // device P3 encoding (rtx_p3.h)
   HostBuf stage_rgb, stage_spp;  // rtx_render_multi: pinned D2H staging of this device's stripes
   HostBuf counters_h;            // timed renders: pinned copy of the statistics counters (read after the end event)
-  HostBuf patch_h;               // adaptive renders with an early output: the patch list (PixelPatch)
-  int64_t patch_n = 0;           // ... its length (0: no patch list; the output came back whole)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<hipEvent_t> evpool;
   // banded output copies (BandSink): a copy stream and its ordering events
@@ -836,11 +829,9 @@ int set_segbuf(unsigned long long* ctr, uint16_t* segs, hipStream_t st) {
 //    or stop; every phase is a launch of its own with its own drain.
 // `mark` records a hot-kernel timing event (before and after each persistent launch);
 // hot_launches counts them.  The caller resolves the pixels (k_resolve).
-// `snap(knext, active)`, when given, is called once before the first phase whose pixels are at
-// most an eighth of the render's (the output's early copy, render_device_impl).
-template <class Mark, class Snap>
+template <class Mark>
 int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const rtx_render_params* prm,
-                    const PixelSoA& px, int budget, hipStream_t s, Mark mark, uint64_t& hot_launches, Snap snap) {
+                    const PixelSoA& px, int budget, hipStream_t s, Mark mark, uint64_t& hot_launches) {
   const int64_t npix = A.npix;
   const int K1 = std::min(std::max(1, prm->min_spp), budget);
   static const bool debug = std::getenv("RTX_DEBUG_ADAPT") != nullptr;  // per-phase slot counts on stderr
@@ -1078,17 +1069,12 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     return launch(2, Lg, Ag, nullptr, 0);
   }
   Lg.map = 1;
-  bool snapped = false;
   for (int g = 2;; g++) {
     // this phase's slot count, computed at the end of the previous one
     HIPC(hipEventSynchronize(w.ev));
     const unsigned long long nsl = ((const volatile unsigned long long*)w.total_h.p)[0];
     const int64_t active = (int64_t)((const volatile unsigned long long*)w.total_h.p)[1];
     if (nsl == 0) break;
-    if (!snapped && active * 8 <= npix) {  // (record(g - 1) wrote this phase's batches to w.k[g & 1])
-      snapped = true;
-      if ((rc = snap((const uint32_t*)w.k[g & 1].as<uint32_t>(), active))) return rc;
-    }
     if ((rc = launch(g, Lg, Ag, w.segs.as<uint16_t>(), active))) return rc;
     if ((rc = record(g, Ag.L, active))) return rc;
   }
@@ -1601,43 +1587,6 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
       sc->band_ev.push_back(e);
     }
   const int wf_grid = std::max(1, std::min<int>(sc->cus * 16, (int)((nslots + kBlock - 1) / kBlock)));
-  // adaptive renders into a sink that takes an early output: once few pixels still sample, the
-  // whole output is resolved and copied to the host (copy stream) while the last phases run;
-  // the pixels sampling then are listed, and their final output comes back as a patch list
-  int64_t patch_n = 0;
-  sc->patch_n = 0;
-  auto snap = [&](const uint32_t* knext, int64_t active) -> int {
-    if (!sink || !sink->early) return RTX_OK;
-    AdaptWs& w = sc->aw;
-    int rc2;
-    if ((rc2 = w.patch_flag.reserve(npix * sizeof(uint32_t)))) return rc2;
-    if ((rc2 = w.patch_pos.reserve(npix * sizeof(uint32_t)))) return rc2;
-    if ((rc2 = w.patch_idx.reserve(std::max<int64_t>(1, active) * sizeof(uint32_t) + sizeof(uint32_t)))) return rc2;
-    if ((rc2 = w.patch_val.reserve(std::max<int64_t>(1, active) * sizeof(PixelPatch)))) return rc2;
-    if ((rc2 = w.scan_tmp.reserve(std::max<size_t>(16, rtxscan::temp_bytes(npix))))) return rc2;
-    hipLaunchKernelGGL(k_resolve, dim3(pix_blocks), dim3(kBlock), 0, s, px, npix, 0, prm->spp, d_rgb, d_spp);
-    HIPC(hipGetLastError());
-    if (!sc->copy_stream) HIPC(hipStreamCreateWithFlags(&sc->copy_stream, hipStreamNonBlocking));
-    while (sc->band_ev.size() < kBands + 1) {
-      hipEvent_t e = nullptr;
-      HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      sc->band_ev.push_back(e);
-    }
-    HIPC(hipEventRecord(sc->band_ev[0], s));
-    HIPC(hipStreamWaitEvent(sc->copy_stream, sc->band_ev[0], 0));
-    if ((rc2 = sink->early(sink->ctx, sc->copy_stream))) return rc2;
-    uint32_t* flag = w.patch_flag.as<uint32_t>();
-    uint32_t* pos = w.patch_pos.as<uint32_t>();
-    hipLaunchKernelGGL(k_tile_flags, dim3(pix_blocks), dim3(kBlock), 0, s, knext, npix, flag);
-    HIPC(hipGetLastError());
-    HIPC(rtxscan::exclusive_scan_u32(flag, pos, npix, w.scan_tmp.p, w.scan_tmp.n, s));
-    uint32_t* idx = w.patch_idx.as<uint32_t>();
-    hipLaunchKernelGGL(k_tile_compact, dim3(pix_blocks), dim3(kBlock), 0, s, (const uint32_t*)flag,
-                       (const uint32_t*)pos, npix, idx, idx + active);
-    HIPC(hipGetLastError());
-    patch_n = active;
-    return RTX_OK;
-  };
   if (phased) {
     if ((rc = render_adaptive(sc, L, A, prm, px, budget, s, [&](hipStream_t st) -> int {
            if (timed) {
@@ -1646,7 +1595,7 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
              HIPC(hipEventRecord(e, st));
            }
            return RTX_OK;
-         }, hot_launches, snap)))
+         }, hot_launches)))
       return rc;
   }
   for (int s0 = 0, Kc = 0; s0 < budget && !phased; s0 += Kc) {
@@ -1781,19 +1730,6 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
                        prm->mode == RTX_MODE_MEGAKERNEL ? (mk_adaptive ? 2 : 1) : 0, prm->spp, d_rgb, d_spp);
     HIPC(hipGetLastError());
   }
-  if (patch_n > 0) {  // the early output's patch list: the final output of the pixels sampling since
-    AdaptWs& w = sc->aw;
-    if ((rc = sc->patch_h.reserve((size_t)patch_n * sizeof(PixelPatch)))) return rc;
-    hipLaunchKernelGGL(k_patch_gather, dim3((unsigned)((patch_n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                       (const uint32_t*)w.patch_idx.as<uint32_t>(), patch_n, (const double*)d_rgb,
-                       (const int32_t*)d_spp, w.patch_val.as<PixelPatch>());
-    HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(sc->patch_h.p, w.patch_val.p, (size_t)patch_n * sizeof(PixelPatch), hipMemcpyDeviceToHost, s));
-    // the caller's stream owns the output again once the early copies are done
-    HIPC(hipEventRecord(sc->band_ev[kBands], sc->copy_stream));
-    HIPC(hipStreamWaitEvent(s, sc->band_ev[kBands], 0));
-    sc->patch_n = patch_n;
-  }
   if (timed) {  // the statistics come back with the frame: one wait on the end event, no blocking copy after it
     if ((rc = sc->counters_h.reserve(18 * sizeof(unsigned long long)))) return rc;
     HIPC(hipMemcpyAsync(sc->counters_h.p, cnt, 18 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
@@ -1910,9 +1846,7 @@ int render_stripes_to_host(rtx_scene* sc, const rtx_camera* cam, const rtx_rende
     bool direct;
     int64_t W, R, N, stripe, full;
     size_t row_rgb;
-    int64_t npix;
-    int (*copy_fn)(void*, int64_t, int64_t, hipStream_t);
-  } ctx{sc, out_rgb, direct, W, R, N, stripe, full, row_rgb, npix, nullptr};
+  } ctx{sc, out_rgb, direct, W, R, N, stripe, full, row_rgb};
   auto copy = [](void* c, int64_t p0, int64_t p1, hipStream_t cs) -> int {
     const Ctx& k = *(const Ctx*)c;
     const double* src = k.sc->out_rgb.as<double>();
@@ -1933,42 +1867,19 @@ int render_stripes_to_host(rtx_scene* sc, const rtx_camera* cam, const rtx_rende
                           src + (size_t)rs * k.W * 3, (size_t)(r1 - rs) * k.row_rgb, hipMemcpyDeviceToHost, cs));
     return RTX_OK;
   };
-  ctx.copy_fn = copy;
-  BandSink sink{R * W, copy, &ctx};
-  // adaptive renders: the whole output (colours, sample counts) early, on the copy stream
-  if ((rc = sc->stage_spp.reserve((size_t)std::max<int64_t>(1, npix) * sizeof(int32_t)))) return rc;
-  sink.early = [](void* c, hipStream_t cs) -> int {
-    const Ctx& k = *(const Ctx*)c;
-    int rc2;
-    if ((rc2 = k.copy_fn(c, 0, k.npix, cs))) return rc2;
-    HIPC(hipMemcpyAsync(k.sc->stage_spp.p, k.sc->out_spp.p, (size_t)k.npix * sizeof(int32_t), hipMemcpyDeviceToHost, cs));
-    return RTX_OK;
-  };
+  const BandSink sink{R * W, copy, &ctx};
   if ((rc = render_device_impl(sc, cam, &q, sc->out_rgb.as<double>(), sc->out_spp.as<int32_t>(), st, sc->stream,
                                &sink)))
     return rc;
   if (npix == 0) return RTX_OK;
-  const int64_t patch_n = sc->patch_n;  // (> 0: the output came back early, the patch list follows)
   // renders the accumulate does not band (adaptive sampling) copy the whole output here
-  if (!sum_path_of(&q) && patch_n == 0 && (rc = copy(&ctx, 0, npix, sc->stream))) return rc;
-  if (out_spp && patch_n == 0)
+  if (!sum_path_of(&q) && (rc = copy(&ctx, 0, npix, sc->stream))) return rc;
+  if (out_spp) {
+    if ((rc = sc->stage_spp.reserve((size_t)npix * sizeof(int32_t)))) return rc;
     HIPC(hipMemcpyAsync(sc->stage_spp.p, sc->out_spp.p, (size_t)npix * sizeof(int32_t), hipMemcpyDeviceToHost,
                         sc->stream));
-  HIPC(hipStreamSynchronize(sc->stream));
-  // the patch list: the final output of the pixels still sampling at the early copy
-  for (int64_t i = 0; i < patch_n; i++) {
-    const PixelPatch& pp = ((const PixelPatch*)sc->patch_h.p)[i];
-    const int64_t p = pp.p, pr = p / W, x = p - pr * W;  // packed row, column
-    double* dst;
-    if (direct) {
-      const int64_t y = (stripe + (pr / R) * N) * R + pr % R;  // image row of packed row pr
-      dst = out_rgb + ((size_t)y * W + x) * 3;
-    } else {
-      dst = (double*)sc->stage_rgb.p + (size_t)p * 3;
-    }
-    dst[0] = pp.rgb[0], dst[1] = pp.rgb[1], dst[2] = pp.rgb[2];
-    ((int32_t*)sc->stage_spp.p)[p] = pp.spp;
   }
+  HIPC(hipStreamSynchronize(sc->stream));
   int64_t r = 0;  // packed row
   for (int64_t b = stripe; b < nblk; b += N) {
     const int64_t y0 = b * R, rows = std::min<int64_t>(R, H - y0);

@@ -1646,24 +1646,6 @@ __global__ void k_slot_block_init(unsigned long long* __restrict__ ctr, int set,
     if (set) ctr[8 * 16] = nslots, ctr[8 * 16 + 2] = smap;
   }
 }
-// Adaptive frames whose output went to the host early (render_adaptive's snapshot): the pixels
-// still sampling then, with their final output.
-struct PixelPatch {
-  uint32_t p;
-  int32_t spp;
-  double rgb[3];
-};
-__global__ __launch_bounds__(kBlock) void k_patch_gather(const uint32_t* __restrict__ idx, int64_t n,
-                                                         const double* __restrict__ rgb,
-                                                         const int32_t* __restrict__ spp, PixelPatch* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t p = idx[i];
-  PixelPatch r;
-  r.p = p, r.spp = spp ? spp[p] : 0;
-  for (int c = 0; c < 3; c++) r.rgb[c] = rgb[3 * (int64_t)p + c];
-  out[i] = r;
-}
 __global__ __launch_bounds__(kBlock) void k_resolve(PixelSoA px, int64_t npix, int megakernel, int spp,
                                                     double* __restrict__ rgb, int32_t* __restrict__ spp_out) {
   // megakernel: 1 = DefaultSampler (divide by spp), 2 = AdaptiveSampler (by the pixel's count)

@@ -362,32 +362,6 @@ def test_render_multi_banded_output_one_device(rtx_mod, scenes):
             assert st["rays_total"] == fst["rays_total"]
 
 
-def test_render_multi_adaptive_early_output(rtx_mod, scenes):
-    """Adaptive persistent frames through render_multi: once few pixels still sample, the whole
-    output goes to the host early (copy stream, during the last phases) and the pixels still
-    sampling then come back as a patch list.  Against rtx_render (one copy at the end): pinned
-    and pageable framebuffers, one and two scenes on the device, a frame where some phase has
-    at most an eighth of the pixels (the bunny) and one where none has (the Cornell box)."""
-    import torch
-
-    for name, cfg, width, spp, depth in (("bunny", "c3_bunny", 96, 200, 20), ("cornell", "cornell", 40, 48, 20)):
-        path, d = scenes(name)
-        cam = rtx_mod.camera(rtx_mod.camera_config(cfg, width=width))
-        npix = cam.image_width * cam.image_height
-        other = rtx_mod.DeviceScene(rtx_mod.HostScene.load(path))
-        kw = dict(seed=61, adaptive=True, mode="persistent", precision="fast")
-        full, fsp, _ = d.render(cam, spp, depth, **kw)
-        assert name != "bunny" or ((fsp < spp).mean() > 0.5 and (fsp > 64).any())
-        for group in ([d], [d, other]):
-            for pinned in (True, False):
-                if pinned:
-                    out = torch.full((npix, 3), -1.0, dtype=torch.float64).pin_memory().numpy()
-                else:
-                    out = np.full((npix, 3), -1.0)
-                rgb, sp, _, _ = rtx_mod.render_multi(group, cam, spp, depth, out=out, **kw)
-                assert np.array_equal(out, full) and np.array_equal(sp, fsp), (name, len(group), pinned)
-
-
 def test_frame_parts_are_bit_identical(rtx_mod, scenes):
     """Fixed-spp frames of one sample group are traced in several launches over consecutive
     pixel ranges (frame parts, the later ones on a second stream, each part's banded accumulate
