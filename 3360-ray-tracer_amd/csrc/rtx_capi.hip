@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <chrono>
 #include <numeric>
 #include <string>
 #include <thread>
@@ -152,6 +153,12 @@ static AdaptTune g_tune{0, 0, 0.0, 0, 0, 0, 0, 0, -1.0, -1, -1.0, 0, -1};
 constexpr int kFirstPassMap = 1;  // the adaptive first pass runs the phase kernel (MAP 1, no slot map)
 // Overrides of kFrameParts / kFrameLastShare (rtx_internal_frame_parts; 0: the default)
 static int g_frame_parts = 0;
+// RTX_DEBUG_HOST: host-side timestamps of a frame (render_stripes_to_host prints them)
+static const bool g_debug_host = std::getenv("RTX_DEBUG_HOST") != nullptr;
+static double host_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static double g_t_launch = 0, g_t_sync0 = 0, g_t_sync1 = 0;
 static double g_frame_last_share = 0.0;
 struct AdaptWs {
   DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer, [134] TileArgs
@@ -1494,6 +1501,7 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     hipLaunchKernelGGL(k_frame_init, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, pz, npix,
                        sum_path ? 0 : 1, sc->counters.as<unsigned long long>(), kCounterWords);
     HIPC(hipGetLastError());
+    if (g_debug_host) g_t_launch = host_us();
   }
   const bool banded = sum_path && sink && npix > 0;
   if (banded) {
@@ -1730,6 +1738,11 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
                        prm->mode == RTX_MODE_MEGAKERNEL ? (mk_adaptive ? 2 : 1) : 0, prm->spp, d_rgb, d_spp);
     HIPC(hipGetLastError());
   }
+  // renders the accumulate does not band (adaptive sampling): the whole output to the sink here,
+  // on the stream before the frame's end event, so one host wait covers the frame and its copy
+  if (sink && !banded && npix > 0) {
+    if ((rc = sink->copy(sink->ctx, 0, npix, s))) return rc;
+  }
   if (timed) {  // the statistics come back with the frame: one wait on the end event, no blocking copy after it
     if ((rc = sc->counters_h.reserve(18 * sizeof(unsigned long long)))) return rc;
     HIPC(hipMemcpyAsync(sc->counters_h.p, cnt, 18 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
@@ -1740,7 +1753,9 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     HIPC(hipStreamWaitEvent(s, sc->band_ev.back(), 0));
   }
   if (timed) {
+    if (g_debug_host) g_t_sync0 = host_us();
     HIPC(hipEventSynchronize(sc->ev[1]));
+    if (g_debug_host) g_t_sync1 = host_us();
     float ms = 0;
     HIPC(hipEventElapsedTime(&ms, sc->ev[0], sc->ev[1]));
     // the hot launches' event pairs are read only now: no host wait inside the frame, so the
@@ -1817,6 +1832,7 @@ namespace {
 // buffer) and are placed at their rows of the whole-frame buffers.
 int render_stripes_to_host(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* base, int stripe,
                            double* out_rgb, int32_t* out_spp, rtx_stats* st) {
+  const double t_in = g_debug_host ? host_us() : 0.0;
   rtx_render_params q = *base;
   q.stripe_index = stripe;
   q.x0 = q.y0 = q.w = q.h = 0;
@@ -1872,8 +1888,7 @@ int render_stripes_to_host(rtx_scene* sc, const rtx_camera* cam, const rtx_rende
                                &sink)))
     return rc;
   if (npix == 0) return RTX_OK;
-  // renders the accumulate does not band (adaptive sampling) copy the whole output here
-  if (!sum_path_of(&q) && (rc = copy(&ctx, 0, npix, sc->stream))) return rc;
+  // (renders the accumulate does not band sent the whole output to the sink at their end)
   if (out_spp) {
     if ((rc = sc->stage_spp.reserve((size_t)npix * sizeof(int32_t)))) return rc;
     HIPC(hipMemcpyAsync(sc->stage_spp.p, sc->out_spp.p, (size_t)npix * sizeof(int32_t), hipMemcpyDeviceToHost,
@@ -1890,6 +1905,14 @@ int render_stripes_to_host(rtx_scene* sc, const rtx_camera* cam, const rtx_rende
       std::memcpy(out_spp + (size_t)y0 * W, (const char*)sc->stage_spp.p + (size_t)r * row_spp,
                   (size_t)rows * row_spp);
     r += rows;
+  }
+  if (g_debug_host) {
+    static double t_prev_out = 0;
+    const double t_out = host_us();
+    fprintf(stderr, "rtx host: since last frame %.1f us | to first launch %.1f | launches %.1f | sync wait %.1f | after %.1f\n",
+            t_prev_out > 0 ? t_in - t_prev_out : -1.0, g_t_launch - t_in, g_t_sync0 - g_t_launch, g_t_sync1 - g_t_sync0,
+            t_out - g_t_sync1);
+    t_prev_out = t_out;
   }
   return RTX_OK;
 }
