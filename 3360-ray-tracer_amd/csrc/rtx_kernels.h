@@ -28,6 +28,9 @@ constexpr int kRefillMin = 24;      // persistent lanes: refill once this many l
 constexpr int kRefillMinPark = 16;  // the same for the PARK kernel
 constexpr int kParkAt = 16;  // PARK kernel: park traversals once at most this many lanes still walk (ab_parkT_*)
 constexpr int kChunk = 256;  // persistent: slots taken per atomic on a region's slot counter (ab_chunk_*)
+#ifndef RTX_REFILL_SHARED
+#define RTX_REFILL_SHARED 0  // > 0: the refill threshold of the block-shared chunk launches (A/B; 0: the kernel's own)
+#endif
 #ifndef RTX_CHUNK_SHARED
 #define RTX_CHUNK_SHARED 128
 #endif
@@ -866,7 +869,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
     // primary-generation code over several lanes.
     const unsigned long long idle = __ballot(!has);
     bool fresh = false;
-    constexpr int kRefill = kPark ? kRefillMinPark : kRefillMin;
+    constexpr int kRefill = kShared && RTX_REFILL_SHARED > 0 ? RTX_REFILL_SHARED : kPark ? kRefillMinPark : kRefillMin;
     if (kTiles) {
       // tile schedule: the idle lanes take slots of the block's tiles in flight (descriptor
       // order; each tile's front batch, then its back batch, laid out here once the front's
