@@ -1321,7 +1321,10 @@ __device__ __forceinline__ uint32_t adapt_next_batch(const double (&mean)[3], co
 // the running count), so the parallelism is across pixels, and each lane streams its own run
 // of the phase's slots with the loads of the next kRecAhead samples in flight while it
 // replays the current one (a lane's run is contiguous: its loads walk the same cache lines).
-constexpr int kRecAhead = 8;
+#ifndef RTX_REC_AHEAD
+#define RTX_REC_AHEAD 8
+#endif
+constexpr int kRecAhead = RTX_REC_AHEAD;
 __global__ __launch_bounds__(kBlock) void k_adapt_record(PixelSoA px, const double* __restrict__ L, int64_t nq,
                                                          int64_t npix, AdaptPlan ap) {
   const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
