@@ -148,8 +148,9 @@ struct AdaptTune {
   double tile_starve;    // tiles: margin growth per idle wave of the block at a record (< 0: default)
   int tile_split;        // tiles: predicted samples above this are split into two batches (0: default; huge: never)
   int first_map;         // the uniform first pass: 1 the phase kernel (block-shared chunks), 0 the uniform-group one (< 0: default)
+  double phase_mstep;    // phases: the batch margin's growth per phase (< 0: kAdaptMarginStep)
 };
-static AdaptTune g_tune{0, 0, 0.0, 0, 0, 0, 0, 0, -1.0, -1, -1.0, 0, -1};
+static AdaptTune g_tune{0, 0, 0.0, 0, 0, 0, 0, 0, -1.0, -1, -1.0, 0, -1, -1.0};
 constexpr int kFirstPassMap = 1;  // the adaptive first pass runs the phase kernel (MAP 1, no slot map)
 // Overrides of kFrameParts / kFrameLastShare (rtx_internal_frame_parts; 0: the default)
 static int g_frame_parts = 0;
@@ -916,7 +917,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ap.kmin = tiles ? tile_kinc
                     : (int32_t)std::min<int64_t>(budget, (phase_slots + active - 1) / std::max<int64_t>(1, active));
     ap.rel = prm->rel_threshold;
-    ap.margin_step = kAdaptMarginStep;
+    ap.margin_step = g_tune.phase_mstep >= 0 ? g_tune.phase_mstep : kAdaptMarginStep;
     ap.segs = !L.count ? nullptr : g == 1 ? sc->segs1.as<uint16_t>() : w.segs.as<uint16_t>();
     ap.rec_segs = A.counters + 9;
     ap.active = ctr + 8 * 16 + 1;
@@ -2137,13 +2138,13 @@ extern "C" int rtx_internal_check_sincos(int device, int64_t n, uint64_t seed, i
 extern "C" int rtx_internal_adapt_tune(int32_t tile_kcap, int32_t tile_kinc, double tile_margin, int64_t phase_slots,
                                        int32_t phase_kcap, int32_t tile_first_pass, int32_t tile_tp, int32_t tile_nt,
                                        double tile_mstep, int32_t tile_tail, double tile_starve, int32_t tile_split,
-                                       int32_t first_map) {
+                                       int32_t first_map, double phase_mstep) {
   if (tile_kcap < 0 || tile_kinc < 0 || !(tile_margin >= 0) || phase_slots < 0 || phase_kcap < 0 ||
       tile_first_pass < 0 || tile_first_pass > 2 || tile_tp < 0 || tile_tp > kTileTP || tile_nt < 0 ||
       tile_nt > kTileNT || tile_split < 0 || first_map > 1)
     return fail(RTX_ERR_INVALID, "bad tuning value");
   g_tune = AdaptTune{tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap, tile_first_pass, tile_tp, tile_nt,
-                     tile_mstep, tile_tail, tile_starve, tile_split, first_map};
+                     tile_mstep, tile_tail, tile_starve, tile_split, first_map, phase_mstep};
   return RTX_OK;
 }
 

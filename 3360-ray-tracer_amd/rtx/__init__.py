@@ -355,19 +355,19 @@ class DeviceScene:
 
 
 def adapt_tune(tile_kcap=0, tile_kinc=0, tile_margin=0.0, phase_slots=0, phase_kcap=0, tile_first_pass=0,
-               tile_tp=0, tile_nt=0, tile_mstep=-1.0, tile_tail=-1, tile_starve=-1.0, tile_split=0, first_map=-1):
+               tile_tp=0, tile_nt=0, tile_mstep=-1.0, tile_tail=-1, tile_starve=-1.0, tile_split=0, first_map=-1, phase_mstep=-1.0):
     """Test / tuning hook (rtx_internal_adapt_tune, not in rtx.h): overrides of the adaptive
     schedules' constants for the renders that follow in this process; no argument (all 0)
     restores the defaults.  Results never depend on them, only the work and the phases do.
     tile_first_pass: 1 the first pass inside the tile launch, 2 a uniform launch of its own.
     first_map: the uniform first pass on the phase kernel (1, block-shared chunks) or on the
-    uniform-group kernel (0)."""
+    uniform-group kernel (0).  phase_mstep: the phases' batch margin growth per phase."""
     f = lib().rtx_internal_adapt_tune
     f.argtypes = [C.c_int32, C.c_int32, C.c_double, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
-                  C.c_double, C.c_int32, C.c_double, C.c_int32, C.c_int32]
+                  C.c_double, C.c_int32, C.c_double, C.c_int32, C.c_int32, C.c_double]
     f.restype = C.c_int
     _check(f(tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap, tile_first_pass, tile_tp, tile_nt,
-             tile_mstep, tile_tail, tile_starve, tile_split, first_map), "rtx_internal_adapt_tune")
+             tile_mstep, tile_tail, tile_starve, tile_split, first_map, phase_mstep), "rtx_internal_adapt_tune")
 
 
 def frame_parts(parts=0, last_share=0.0):

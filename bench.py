@@ -174,7 +174,7 @@ def main():
         rtx.frame_parts(int(fp[0]), float(fp[1]) if len(fp) > 1 else 0.0)
     if args.adapt_tune:
         kv = dict(x.split("=") for x in args.adapt_tune.split(","))
-        rtx.adapt_tune(**{k: (float(v) if k in ("tile_margin", "tile_mstep", "tile_starve") else int(v)) for k, v in kv.items()})
+        rtx.adapt_tune(**{k: (float(v) if k in ("tile_margin", "tile_mstep", "tile_starve", "phase_mstep") else int(v)) for k, v in kv.items()})
     workload = args.workload if args.workload != "auto" else ("c3_bunny" if world == 1 else "c4_bunny4k")
     scene_name, preset, width, spp, depth = WORKLOADS[workload]
     spp = args.spp or spp
