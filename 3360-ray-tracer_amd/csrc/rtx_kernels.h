@@ -27,7 +27,10 @@ constexpr int kSlotTargetLog2 = 29;  // persistent: up to 2^29 slots (pixel x sa
 constexpr int kRefillMin = 24;      // persistent lanes: refill once this many lanes of a wave are idle (ab_refill2_*)
 constexpr int kRefillMinPark = 16;  // the same for the PARK kernel
 constexpr int kParkAt = 16;  // PARK kernel: park traversals once at most this many lanes still walk (ab_parkT_*)
-constexpr int kChunk = 256;  // persistent: slots taken per atomic on a region's slot counter (ab_chunk_*)
+#ifndef RTX_CHUNK
+#define RTX_CHUNK 256
+#endif
+constexpr int kChunk = RTX_CHUNK;  // persistent: slots taken per atomic on a region's slot counter (ab_chunk_*)
 #ifndef RTX_REFILL_SHARED
 #define RTX_REFILL_SHARED 0  // > 0: the refill threshold of the block-shared chunk launches (A/B; 0: the kernel's own)
 #endif
