@@ -477,6 +477,7 @@ std::vector<T> read_bin(const std::string& path) {
 // materials, PixelState and write_color.  Tile = full image.  Writes:
 //   <out>.ppm      the P3 text PPM exactly as Render() would print it
 //   <out>.f64      linear framebuffer sum/(float)samples, doubles, row-major RGB
+//   <out>.spp      samples per pixel (int32);  <out>.var  per-pixel sample variance m2/(n-1), RGB
 //   <out>.stats    rays (segments submitted to IntersectBatch), primaries, samples per pixel
 void render_wavefront(RefScene& S, Cam& cam, int max_depth, int max_spp, int batch, bool adaptive,
                       const std::string& out) {
@@ -591,7 +592,7 @@ void render_wavefront(RefScene& S, Cam& cam, int max_depth, int max_spp, int bat
     }
   }
   const auto t_loop = std::chrono::steady_clock::now();
-  std::vector<double> fb(3 * (size_t)N);
+  std::vector<double> fb(3 * (size_t)N), var(3 * (size_t)N);
   std::vector<int> spp(N);
   std::ofstream ppm(out + ".ppm");
   ppm << "P3\n" << W << ' ' << H << "\n255\n";
@@ -601,9 +602,14 @@ void render_wavefront(RefScene& S, Cam& cam, int max_depth, int max_spp, int bat
     fb[3 * i + 1] = c.y();
     fb[3 * i + 2] = c.z();
     spp[i] = px[i].samples;
+    const Color v = integrator::Variance(px[i]);  // pixel_state.h:41-49, for the statistical parity test
+    var[3 * i] = v.x();
+    var[3 * i + 1] = v.y();
+    var[3 * i + 2] = v.z();
     core::write_color(ppm, c);
   }
   write_bin(out + ".f64", fb);
+  write_bin(out + ".var", var);
   write_bin(out + ".spp", spp);
   ppm.close();
   const auto t_end = std::chrono::steady_clock::now();
@@ -927,7 +933,9 @@ int main(int argc, char** argv) {
   } else if (cmd == "render" && argc == 23) {
     auto S = load_scene(argv[2], argv[3]);
     Cam cam = parse_cam(argv + 4);
-    core::SeedRng((unsigned)std::strtoul(argv[21], nullptr, 10));
+    // seed "random": the main thread keeps its random_device seed too, as the reference runs
+    // the bunny scene (no SeedRng call on that path; random.h:14-17)
+    if (std::string(argv[21]) != "random") core::SeedRng((unsigned)std::strtoul(argv[21], nullptr, 10));
     render_wavefront(*S, cam, std::atoi(argv[18]), std::atoi(argv[19]), 2 * 8192, std::atoi(argv[20]) != 0,
                      argv[22]);
   } else if (cmd == "megakernel" && argc == 22) {

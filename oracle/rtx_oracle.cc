@@ -850,7 +850,7 @@ bool shade(const Scene& S, const Params& P, PathState& ps, const Hit& rec, bool 
 // the draw order is exactly the reference's single-thread order; in philox mode it must
 // give the same result as render_per_pixel (order independence check).
 void render_wavefront(const Scene& S, const Camera& cam, const Params& P, double* fb, int* spp_out,
-                      Stats& st) {
+                      Stats& st, double* var_out) {
   const int W = cam.width, H = cam.height, N = W * H;
   std::mt19937 mt(P.seed);
   std::uniform_real_distribution<double> dist(0.0, 1.0);
@@ -901,6 +901,8 @@ void render_wavefront(const Scene& S, const Camera& cam, const Params& P, double
     double inv = px[i].samples > 0 ? 1.0 / (double)(float)px[i].samples : 0.0;
     for (int c = 0; c < 3; c++) fb[3 * (size_t)i + c] = px[i].samples > 0 ? inv * px[i].sum[c] : 0.0;
     if (spp_out) spp_out[i] = px[i].samples;
+    if (var_out)
+      for (int c = 0; c < 3; c++) var_out[3 * (size_t)i + c] = px[i].samples > 1 ? px[i].m2[c] / (px[i].samples - 1) : 0.0;
   }
 }
 
@@ -909,7 +911,7 @@ void render_wavefront(const Scene& S, const Camera& cam, const Params& P, double
 // pass, wavefront.cc:57-79).  Parallel over pixels (OpenMP), result independent of the
 // thread count.
 void render_per_pixel(const Scene& S, const Camera& cam, const Params& P, double* fb, int* spp_out,
-                      Stats& st) {
+                      Stats& st, double* var_out) {
   const int W = cam.width;
   const int tw = P.w, th = P.h;
   const int min_spp = P.adaptive ? P.min_spp : (1 << 30);
@@ -943,6 +945,8 @@ void render_per_pixel(const Scene& S, const Camera& cam, const Params& P, double
       double inv = ps.samples > 0 ? 1.0 / (double)(float)ps.samples : 0.0;
       for (int c = 0; c < 3; c++) fb[3 * o + c] = ps.samples > 0 ? inv * ps.sum[c] : 0.0;
       if (spp_out) spp_out[o] = ps.samples;
+      if (var_out)
+        for (int c = 0; c < 3; c++) var_out[3 * o + c] = ps.samples > 1 ? ps.m2[c] / (ps.samples - 1) : 0.0;
     }
   }
   st.rays += rays;
@@ -1380,7 +1384,11 @@ int orc_camera_init(orc_camera* c, double* basis /* 21: center p00 du dv u v w *
 }
 // fb: tile w*h*3 doubles (whole image in wavefront mode), spp: tile w*h ints (may be NULL)
 // stats: [rays, primaries]
-int orc_render(void* sp, orc_camera* c, const orc_params* p, double* fb, int* spp, long long* stats) {
+// orc_render_var: orc_render plus each pixel's sample variance m2/(n-1) per channel
+// (pixel_state.h:41-49) in var[3 * pixel] (wavefront and per-pixel modes), for the
+// statistical parity test against the reference as it runs (tests/test_statistical_parity.py)
+int orc_render_var(void* sp, orc_camera* c, const orc_params* p, double* fb, int* spp, long long* stats,
+                   double* var) {
   Scene* s = (Scene*)sp;
   Camera cam;
   cam.aspect = c->aspect, cam.vfov = c->vfov, cam.defocus = c->defocus, cam.focus = c->focus;
@@ -1399,19 +1407,22 @@ int orc_render(void* sp, orc_camera* c, const orc_params* p, double* fb, int* sp
     return -1;
   }
   Stats st;
-  if (p->mode == 0) render_wavefront(*s, cam, P, fb, spp, st);
+  if (p->mode == 0) render_wavefront(*s, cam, P, fb, spp, st, var);
   else if (p->mode == 1) {
     if (P.rng_mode != 1) {
       g_err = "per-pixel mode needs philox";
       return -1;
     }
-    render_per_pixel(*s, cam, P, fb, spp, st);
+    render_per_pixel(*s, cam, P, fb, spp, st, var);
   } else {
     P.mk_min_samples = p->mk_min_samples, P.mk_threshold = p->mk_threshold;
     render_megakernel(*s, cam, P, fb, spp, st);
   }
   stats[0] = st.rays, stats[1] = st.primaries;
   return 0;
+}
+int orc_render(void* sp, orc_camera* c, const orc_params* p, double* fb, int* spp, long long* stats) {
+  return orc_render_var(sp, c, p, fb, spp, stats, nullptr);
 }
 // Philox stream check for the GPU RNG: out[i] = RandomDouble for (seed, pixel, sample,
 // stream, draw = i)

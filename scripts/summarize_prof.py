@@ -111,7 +111,10 @@ def valu_profile(d, k, v, launches, hbm_per_launch, rnd, tag, workload, mode, pr
                       " / segments; hbm = (FETCH_SIZE x 2 + WRITE_SIZE) x 1 KiB / segments"}
     for c in ("GRBM_GUI_ACTIVE", "SQ_WAVE_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
               "SQ_ACTIVE_INST_ANY", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_LDS",
-              "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64"):
+              "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64",
+              "SQ_ACTIVE_INST_VALU2", "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64",
+              "SQ_INSTS_VALU_CVT", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_FMA_F32",
+              "SQ_WAVES"):
         if c in v:
             out[c.lower() + "_per_launch"] = per_launch(v, launches, k, c)
     json.dump(out, open(os.path.join(ROOT, "profiles", f"valu_{workload}_{mode}_{prec}.json"), "w"), indent=1)

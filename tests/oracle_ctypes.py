@@ -55,6 +55,8 @@ def lib():
         L.orc_camera_init.argtypes = [C.POINTER(OrcCamera), C.c_void_p]
         L.orc_render.argtypes = [C.c_void_p, C.POINTER(OrcCamera), C.POINTER(OrcParams), C.c_void_p, C.c_void_p,
                                  C.c_void_p]
+        L.orc_render_var.argtypes = [C.c_void_p, C.POINTER(OrcCamera), C.POINTER(OrcParams), C.c_void_p,
+                                     C.c_void_p, C.c_void_p, C.c_void_p]
         L.orc_philox.argtypes = [C.c_ulonglong, C.c_uint, C.c_uint, C.c_int, C.c_void_p]
         L.orc_philox_stream.argtypes = [C.c_ulonglong, C.c_uint, C.c_uint, C.c_uint, C.c_int, C.c_void_p]
         L.orc_write_ppm.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p]
@@ -127,7 +129,7 @@ class Scene:
         return out[:min(n, cap)], n
 
     def render(self, cam_cfg, width, spp, max_depth, seed, adaptive=1, rng="philox", mode="per_pixel",
-               tile=None, threads=1, mk_min_samples=0, mk_threshold=0.0):
+               tile=None, threads=1, mk_min_samples=0, mk_threshold=0.0, variance=False):
         """mode="megakernel": adaptive=0 is DefaultSampler(spp); adaptive=1 is
         AdaptiveSampler(mk_min_samples, spp, mk_threshold) (sampler.h:44-82)."""
         cam = make_camera(cam_cfg, width)
@@ -148,10 +150,15 @@ class Scene:
         fb = np.zeros((h, w, 3))
         spp_out = np.zeros((h, w), np.int32)
         stats = np.zeros(2, np.int64)
-        rc = lib().orc_render(self.h, C.byref(cam), C.byref(p), _ptr(fb), _ptr(spp_out), _ptr(stats))
+        var = np.zeros((h, w, 3)) if variance else None
+        rc = lib().orc_render_var(self.h, C.byref(cam), C.byref(p), _ptr(fb), _ptr(spp_out), _ptr(stats),
+                                  _ptr(var) if variance else None)
         if rc != 0:
             raise RuntimeError(lib().orc_last_error().decode())
-        return fb, spp_out, {"rays": int(stats[0]), "primaries": int(stats[1])}
+        st = {"rays": int(stats[0]), "primaries": int(stats[1])}
+        if variance:  # per-pixel sample variance m2/(n-1) (pixel_state.h:41-49)
+            st["variance"] = var
+        return fb, spp_out, st
 
 
 def aabb(cases):
