@@ -16,11 +16,29 @@
 #include <vector>
 
 #include "rtx.h"
-#include "rtx_kernels.h"
+#include "rtx_frame_kernels.h"
 #include "rtx_p3.h"
 #include "rtx_scan.h"
 
 using namespace rtxd;
+
+// The PARK instantiations of k_persistent are compiled in rtx_park.hip (RTX_PARK_TU).
+namespace rtxd {
+#define RTX_PARK_EXTERN(ST, CO, SC, MP, PK)                                                                   \
+  extern template __global__ void k_persistent<ST, true, CO, SC, PK, -1, false, false, false, MP>(RenderArgs, \
+                                                                                              unsigned long long*);
+RTX_PARK_INSTANCES(RTX_PARK_EXTERN)
+#undef RTX_PARK_EXTERN
+#define RTX_PARK_TRI_EXTERN(ST, MP, PK)                                                                             \
+  extern template __global__ void k_persistent<ST, true, false, false, PK, RTX_PRIM_TRIANGLE, false, false, false, \
+                                               MP>(RenderArgs, unsigned long long*);                              \
+  extern template __global__ void k_persistent<ST, true, false, false, PK, RTX_PRIM_TRIANGLE, true, false, false,  \
+                                               MP>(RenderArgs, unsigned long long*);                              \
+  extern template __global__ void k_persistent<ST, true, false, false, PK, RTX_PRIM_TRIANGLE, true, true, false,   \
+                                               MP>(RenderArgs, unsigned long long*);
+RTX_PARK_TRI_INSTANCES(RTX_PARK_TRI_EXTERN)
+#undef RTX_PARK_TRI_EXTERN
+}  // namespace rtxd
 
 namespace {
 
@@ -94,18 +112,10 @@ float round_up(double x) {
 
 }  // namespace
 
-// Fixed-spp frames traced in one sample group may be split into several launches over
-// consecutive pixel ranges (render_device_impl, "frame parts"; rtx_internal_frame_parts), the
-// last part taking kFrameLastShare of the pixels.  Off by default: each part's launch ends in
-// a drain of its own, and the next part's workgroups do not fill it (C3: one launch 17.01 ms,
-// two parts 17.92-18.43, three 19.30, four 20.03; profiles/r04/ab_frame_parts_r5i_c3.txt).
-constexpr int kFrameParts = 1;
-constexpr double kFrameLastShare = 0.25;
-constexpr int kMaxFrameParts = 4;
-// statistics, queue counts, then one slot counter block per frame part (8 region counters 128 B
-// apart, [128 + 4] the segment buffer (0), ...)
+// statistics, queue counts, then the slot counter block (8 region counters 128 B apart, [128 + 4]
+// the segment buffer (0), ...)
 constexpr int kSlotBlockWords = 8 * 16 + 8;
-constexpr int kCounterWords = 64 + kMaxFrameParts * kSlotBlockWords;
+constexpr int kCounterWords = 64 + kSlotBlockWords;
 
 // Where a render's output goes once a band of it is final (fixed-spp renders): the
 // accumulate of the last sample group runs in kBands bands of the frame's pixels, and after
@@ -122,56 +132,31 @@ constexpr int kBands = 8;  // bands of the last accumulate and of the D2H copies
 // Adaptive renders in phases (render_adaptive)
 constexpr int64_t kAdaptPhaseSlots = 1 << 23;  // render_adaptive: smallest phase planned while pixels remain (ab r3x/r3y: 2^21..2^25)
 constexpr double kAdaptMarginStep = 0.25;      // render_adaptive: batch margin 1 + step * (phase - 1) (0.5: within noise, r3y)
-// The tile schedule (rtx_kernels.h, TileArgs): the largest batch of one pixel, the smallest
-// further batch of a pixel not yet converged, and the batch margin over the predicted need.
-constexpr int kTileKcap = 128;
-constexpr int kTileKinc = 8;
-constexpr double kTileMargin = 1.0;
-constexpr bool kTileFirstPassInLaunch = false;  // the first pass inside the tile launch (else a uniform launch of its own)
-constexpr int kTileTPDefault = 8, kTileNTDefault = 8;  // pixels per tile, tiles in flight per workgroup
-constexpr int kTileSplit = 8;  // a pixel's predicted samples above this go in two pipelined batches
-constexpr double kTileMarginStep = 0.0;  // the margin's growth per batch of a tile
-constexpr int kTileTail = 0;             // pixels left in a tile that take the rest of their budget at once
-constexpr double kTileStarveGain = 0.0;  // margin growth per idle wave of the block at a record
 // Overrides of the adaptive schedules' constants (0: the default): rtx_internal_adapt_tune, a
 // test and tuning hook (not in rtx.h) that forces small workspaces and floors, so the paths
 // that only a large frame at a large budget reaches run on small frames too.
 struct AdaptTune {
-  int tile_kcap, tile_kinc;
-  double tile_margin;
   int64_t phase_slots;  // phases: the smallest phase planned while pixels remain (kAdaptPhaseSlots)
   int phase_kcap;       // phases: the largest batch of one pixel (else from the workspace)
-  int tile_first_pass;  // tiles: 1 the first pass in the tile launch too, 2 in a launch of its own (0: default)
-  int tile_tp, tile_nt;  // tiles: pixels per tile, tiles in flight per workgroup (0: default)
-  double tile_mstep;     // tiles: margin growth per batch (< 0: default)
-  int tile_tail;         // tiles: pixels left that take the rest of their budget (< 0: default)
-  double tile_starve;    // tiles: margin growth per idle wave of the block at a record (< 0: default)
-  int tile_split;        // tiles: predicted samples above this are split into two batches (0: default; huge: never)
   int first_map;         // the uniform first pass: 1 the phase kernel (block-shared chunks), 0 the uniform-group one (< 0: default)
   double phase_mstep;    // phases: the batch margin's growth per phase (< 0: kAdaptMarginStep)
 };
-static AdaptTune g_tune{0, 0, 0.0, 0, 0, 0, 0, 0, -1.0, -1, -1.0, 0, -1, -1.0};
+static AdaptTune g_tune{0, 0, -1, -1.0};
 constexpr int kFirstPassMap = 1;  // the adaptive first pass runs the phase kernel (MAP 1, no slot map)
-// Overrides of kFrameParts / kFrameLastShare (rtx_internal_frame_parts; 0: the default)
-static int g_frame_parts = 0;
-// RTX_DEBUG_HOST: host-side timestamps of a frame (render_stripes_to_host prints them)
+// RTX_DEBUG_HOST: host-side timestamps of a frame (render_stripes_to_host prints them, with the
+// device; per thread: rtx_render_multi renders each device on a thread of its own)
 static const bool g_debug_host = std::getenv("RTX_DEBUG_HOST") != nullptr;
 static double host_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
-static double g_t_launch = 0, g_t_sync0 = 0, g_t_sync1 = 0;
-static double g_frame_last_share = 0.0;
+static thread_local double g_t_launch = 0, g_t_sync0 = 0, g_t_sync1 = 0;
 struct AdaptWs {
-  DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer, [134] TileArgs
+  DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer
   DevBuf segs;                                  // counting renders: each slot's path segments (u16)
-  // the tile schedule: active pixels, the claim-order sort's keys / values (in, out) and its
-  // temporary storage, per-region tile counts [0..8) + active pixel count [8], TileArgs
-  DevBuf act, tkeys[2], tvals[2], sort_tmp, tcount, targs;
   HostBuf total_h;                              // pinned copy of the next phase's slot count
   hipEvent_t ev = nullptr;                      // total_h written
   void release() {
-    for (DevBuf* b : {&lbuf, &smap, &k[0], &k[1], &off, &scan_tmp, &ctr, &segs, &act, &tkeys[0], &tkeys[1], &tvals[0],
-                      &tvals[1], &sort_tmp, &tcount, &targs})
+    for (DevBuf* b : {&lbuf, &smap, &k[0], &k[1], &off, &scan_tmp, &ctr, &segs})
       b->release();
     total_h.release();
     if (ev) (void)hipEventDestroy(ev);
@@ -204,10 +189,6 @@ struct rtx_scene {
   // banded output copies (BandSink): a copy stream and its ordering events
   hipStream_t copy_stream = nullptr;
   std::vector<hipEvent_t> band_ev;
-  // frame parts after the first: their stream, and events (setup done, each part's end, the
-  // part stream's work done)
-  hipStream_t part_stream = nullptr;
-  std::vector<hipEvent_t> part_ev;
   AdaptWs aw;  // adaptive phases' workspace
   double slot_mem = -1.0;  // bytes the slot buffers may take (slot_target; -1: not yet queried)
   ~rtx_scene() {
@@ -215,9 +196,7 @@ struct rtx_scene {
     aw.release();
     for (auto e : evpool) (void)hipEventDestroy(e);
     for (auto e : band_ev) (void)hipEventDestroy(e);
-    for (auto e : part_ev) (void)hipEventDestroy(e);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
-    if (part_stream) (void)hipStreamDestroy(part_stream);
     (void)hipSetDevice(device);
     for (DevBuf* b : {&nodes, &prims, &mats, &texs, &images, &fnodes, &tri_n, &px_sum, &px_mean, &px_m2, &px_samples,
                       &px_conv, &lbuf, &queue[0], &queue[1], &counters, &out_rgb, &out_spp, &rays, &hits, &p3_scratch,
@@ -406,62 +385,6 @@ int build_fast4(const rtx_bvh_node* n, const rtx_prim* prims, std::vector<F4Node
   }
   return need;
 }
-
-// RTX_QNODE: each F4Node quantised into one 64-byte QNode (rtx_device.h): per axis the origin is
-// the smallest live lower plane and the step the smallest power of two with 254 steps covering
-// the planes; every lower plane byte is the largest q with fmaf(q, s, o) <= the f32 plane and
-// every upper one the smallest q with fmaf(q, s, o) >= it, the device's own decode (one
-// rounding), so the decoded box contains the f32 box.  false: a non-finite plane.
-#if RTX_QNODE
-static bool quantise_f4(const std::vector<F4Node>& f4, std::vector<QNode>& out) {
-  out.assign(f4.size(), QNode{});
-  for (size_t i = 0; i < f4.size(); i++) {
-    const F4Node& f = f4[i];
-    QNode& q = out[i];
-    for (int c = 0; c < 4; c++) q.child[c] = f.child[c];
-    const float* lo[3] = {f.lox, f.loy, f.loz};
-    const float* hi[3] = {f.hix, f.hiy, f.hiz};
-    for (int a = 0; a < 3; a++) {
-      float mn = INFINITY, mx = -INFINITY;
-      for (int c = 0; c < 4; c++)
-        if (lo[a][c] <= hi[a][c]) mn = std::min(mn, lo[a][c]), mx = std::max(mx, hi[a][c]);
-      q.qlo[a] = 0xFFFFFFFFu, q.qhi[a] = 0u;  // every slot empty until set
-      if (mn > mx) {  // no live slot
-        q.o[a] = 0.0f, q.s[a] = 1.0f;
-        continue;
-      }
-      if (!std::isfinite(mn) || !std::isfinite(mx)) return false;
-      const double ext = (double)mx - (double)mn;
-      int e = ext > 0 ? std::ilogb(ext / 254.0) : -126;
-      e = std::max(-126, e);
-      for (;; e++) {
-        if (e > 127) return false;
-        const float st = std::ldexp(1.0f, e);
-        bool ok = true;
-        uint32_t wl = 0, wh = 0;
-        for (int c = 0; c < 4 && ok; c++) {
-          uint32_t bl = 255u, bh = 0u;
-          if (lo[a][c] <= hi[a][c]) {
-            int ql = (int)std::floor(((double)lo[a][c] - mn) / st);
-            ql = std::max(0, std::min(255, ql));
-            while (ql > 0 && std::fmaf((float)ql, st, mn) > lo[a][c]) ql--;
-            int qh = (int)std::ceil(((double)hi[a][c] - mn) / st);
-            qh = std::max(0, std::min(255, qh));
-            while (qh < 255 && std::fmaf((float)qh, st, mn) < hi[a][c]) qh++;
-            ok = std::fmaf((float)ql, st, mn) <= lo[a][c] && std::fmaf((float)qh, st, mn) >= hi[a][c];
-            bl = (uint32_t)ql, bh = (uint32_t)qh;
-          }
-          wl |= bl << (8 * c), wh |= bh << (8 * c);
-        }
-        if (!ok) continue;
-        q.o[a] = mn, q.s[a] = st, q.qlo[a] = wl, q.qhi[a] = wh;
-        break;
-      }
-    }
-  }
-  return true;
-}
-#endif
 
 // Fast-path tree of our own: binned SAH on all three axes (32 bins)
 // over the conservative primitive boxes (prim_box), split down to one primitive per leaf;
@@ -666,23 +589,6 @@ int64_t subset_pixels(const rtx_camera* cam, const rtx_render_params* p, PixelMa
   return (int64_t)m.w * m.h;
 }
 
-// The pixels of map from its local pixel p0 on (p0 a whole number of its rows: stripes of
-// srows rows, or rows of the rectangle), as a map of their own: PixelMap::xy of local pixel i
-// of the result is xy of p0 + i of map.
-PixelMap sub_map(const PixelMap& m, int64_t p0) {
-  PixelMap r = m;
-  if (m.stripes) {
-    const int64_t r0 = p0 / m.W;  // a multiple of srows
-    r.sidx = m.sidx + (int32_t)(r0 / m.srows) * m.scount;
-    r.h = m.h - (int32_t)r0;
-  } else {
-    const int64_t r0 = p0 / std::max(1, m.w);
-    r.y0 = m.y0 + (int32_t)r0;
-    r.h = m.h - (int32_t)r0;
-  }
-  return r;
-}
-
 template <int STACK, bool FAST>
 int launch_intersect(rtx_scene* sc, const rtx_ray* d_rays, int64_t n, rtx_hit* d_hits, double tmin, double tmax,
                      hipStream_t s) {
@@ -708,8 +614,7 @@ struct Launch {
   bool fast, count;
   int park = 0;  // persistent: 0 plain kernel, PARK kernel (parked traversals) with 1 the leaf-step, 2 the speculative walk
   bool generic = false;  // RTX_FLAG_GENERIC: no per-scene specialisation (TK, LAMB, NOTEX, NODOF)
-  int map = 0;           // k_persistent MAP: 0 uniform groups, 1 an adaptive phase's slot map, 2 adaptive tiles
-  int max_grid = 0;      // > 0: at most this many blocks (the tile schedule's workspace has room for them)
+  int map = 0;           // k_persistent MAP: 0 uniform groups, 1 an adaptive phase's slot map
   mutable uint32_t build = 0;  // RTX_BUILD_* bits of the persistent instantiation launched last
 };
 
@@ -731,7 +636,6 @@ int run_persistent_k1(const Launch& L, const RenderArgs& A, unsigned long long* 
   const size_t lds = persist_lds(A.stack_slots, spec_walk(PARK, FAST, SCATTER), block_region_kind(MAP, SCATTER)).end;
   int grid = persistent_grid(
       L.sc, (const void*)k_persistent<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF, MAP>, lds);
-  if (L.max_grid > 0) grid = std::min(grid, L.max_grid);
   L.build = (PARK ? RTX_BUILD_PARK : 0u) | (PARK == 2 ? RTX_BUILD_SPECULATIVE : 0u) | (TK == (int)RTX_PRIM_SPHERE ? RTX_BUILD_SPHERE_TREE : 0u) |
             (TK == (int)RTX_PRIM_TRIANGLE ? RTX_BUILD_TRIANGLE_TREE : 0u) | (LAMB ? RTX_BUILD_LAMBERTIAN : 0u) |
             (NOTEX ? RTX_BUILD_NO_TEXTURES : 0u) | (NODOF ? RTX_BUILD_NO_DEFOCUS : 0u) |
@@ -744,15 +648,12 @@ int run_persistent_k1(const Launch& L, const RenderArgs& A, unsigned long long* 
   HIPC(hipGetLastError());
   return RTX_OK;
 }
-// adaptive renders draw their slots from a slot map or the tile schedule (L.map; never with the
-// scatter API)
+// adaptive renders draw their slots from a slot map (L.map; never with the scatter API)
 template <int STACK, bool FAST, bool COUNT, bool SCATTER, int PARK, int TK, bool LAMB = false, bool NOTEX = false,
           bool NODOF = false>
 int run_persistent_k0(const Launch& L, const RenderArgs& A, unsigned long long* next_slot) {
   if (!SCATTER && L.map == 1)
     return run_persistent_k1<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF, SCATTER ? 0 : 1>(L, A, next_slot);
-  if (!SCATTER && L.map == 2)
-    return run_persistent_k1<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF, SCATTER ? 0 : 2>(L, A, next_slot);
   if (L.map) return fail(RTX_ERR_INVALID, "slot maps are not used with the scatter API");
   return run_persistent_k1<STACK, FAST, COUNT, SCATTER, PARK, TK, LAMB, NOTEX, NODOF, 0>(L, A, next_slot);
 }
@@ -826,15 +727,10 @@ int set_segbuf(unsigned long long* ctr, uint16_t* segs, hipStream_t st) {
 // Adaptive sampling on the persistent kernel: the reference's WavefrontRenderer::Render loop
 // (wavefront.cc:57-225, always adaptive) with the same per-pixel results, on the caller's
 // stream `s`.  Phase 1 traces min_spp samples of every pixel (one uniform launch) and
-// k_adapt_record replays them and sizes each pixel's next batch.  Then either
-//  * tiles (RTX_FLAG_ADAPT_TILES; rtx_kernels.h "tile schedule"): the pixels still sampling are cut into
-//    tiles, ordered per region largest predicted work first (flag, scan, compact, keys, radix
-//    sort: all on the stream, no host round trip), and ONE more persistent launch runs every
-//    further phase of every tile, each tile's record inside the workgroup that traces it; or
-//  * phases (the default; round 3's schedule): after each phase, record + next batch
-//    sizes (k_adapt_record, k_adapt_floor); before each phase, prefix sum and slot map
-//    (k_adapt_expand); the host reads the next phase's slot count (one pinned word) to launch it
-//    or stop; every phase is a launch of its own with its own drain.
+// k_adapt_record replays them and sizes each pixel's next batch.  After each phase, record +
+// next batch sizes (k_adapt_record, k_adapt_floor); before each phase, prefix sum and slot map
+// (k_adapt_expand); the host reads the next phase's slot count (one pinned word) to launch it
+// or stop; every phase is a launch of its own with its own drain.
 // `mark` records a hot-kernel timing event (before and after each persistent launch);
 // hot_launches counts them.  The caller resolves the pixels (k_resolve).
 template <class Mark>
@@ -843,45 +739,19 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   const int64_t npix = A.npix;
   const int K1 = std::min(std::max(1, prm->min_spp), budget);
   static const bool debug = std::getenv("RTX_DEBUG_ADAPT") != nullptr;  // per-phase slot counts on stderr
-  const bool tiles = (prm->flags & RTX_FLAG_ADAPT_TILES) && !(prm->flags & RTX_FLAG_ADAPT_PHASES);
   const int64_t phase_slots = g_tune.phase_slots > 0 ? g_tune.phase_slots : kAdaptPhaseSlots;
   if ((int64_t)npix * K1 > 0xFFFFFFFFll) return fail(RTX_ERR_INVALID, "adaptive render: npix x min_spp above 2^32");
   AdaptWs& w = sc->aw;
   int rc;
-  // tile schedule: room for every block the launch can hold (4 per CU at 128 VGPRs), each with
-  // kTileNT tiles of kTileTP pixels x kcap slots (24 B of radiance each)
-  const int64_t max_blocks = 4ll * sc->cus;
-  const int tp = std::max(1, std::min(kTileTP, g_tune.tile_tp > 0 ? g_tune.tile_tp : kTileTPDefault));
-  const int ntl = std::max(1, std::min(kTileNT, g_tune.tile_nt > 0 ? g_tune.tile_nt : kTileNTDefault));
-  const int64_t max_tiles = (npix + tp - 1) / tp;
-  const bool one_launch = tiles && (g_tune.tile_first_pass ? g_tune.tile_first_pass == 1 : kTileFirstPassInLaunch);
   // the uniform first pass's radiance (and segment) records, in the scene's buffers
-  const double first_bytes = one_launch ? 0.0 : (double)npix * K1 * (3 * sizeof(double) + (L.count ? 2 : 0));
-  int32_t kcap;
-  if (tiles) {
-    kcap = std::max(1, std::min(budget, g_tune.tile_kcap > 0 ? g_tune.tile_kcap : kTileKcap));
-    // within the allowance: a pixel's batches get smaller, not the launch
-    const int64_t per_k = max_blocks * ntl * 2 * tp * (int64_t)(3 * sizeof(double) + (L.count ? 2 : 0));
-    kcap = (int32_t)std::min<int64_t>(kcap, slot_target(sc, per_k, kcap, first_bytes));
-    const int64_t slots = max_blocks * ntl * 2 * tp * (int64_t)kcap;  // two batch buffers per tile
-    if ((rc = w.lbuf.reserve(slots * 3 * sizeof(double)))) return rc;
-    if (L.count && (rc = w.segs.reserve(slots * sizeof(uint16_t)))) return rc;
-    for (DevBuf* b : {&w.k[0], &w.k[1], &w.off, &w.act})
-      if ((rc = b->reserve(npix * sizeof(uint32_t)))) return rc;
-    for (DevBuf* b : {&w.tkeys[0], &w.tkeys[1], &w.tvals[0], &w.tvals[1]})
-      if ((rc = b->reserve(std::max<int64_t>(1, max_tiles) * sizeof(uint32_t)))) return rc;
-    if ((rc = w.scan_tmp.reserve(std::max<size_t>(16, rtxscan::temp_bytes(npix))))) return rc;
-    if ((rc = w.sort_tmp.reserve(std::max<size_t>(16, rtxscan::sort_temp_bytes(max_tiles))))) return rc;
-    if ((rc = w.tcount.reserve(16 * sizeof(uint32_t)))) return rc;
-    if ((rc = w.targs.reserve(sizeof(TileArgs)))) return rc;
-    if ((rc = w.ctr.reserve(8 * 16 * sizeof(unsigned long long) + 64))) return rc;
-  } else {
-    // slots after the first phase: 24 B of radiance + 8 B of slot map each (+ 2 B of segments)
-    const int64_t cap =
-        std::min<int64_t>(0xFFFFFFFFll, slot_target(sc, 32 + (L.count ? 2 : 0), 1ll << kSlotTargetLog2, first_bytes));
-    if (npix * 4 > cap) return fail(RTX_ERR_NOMEM, "adaptive render: too many pixels for the device memory");
-    kcap = (int32_t)std::min<int64_t>(budget, std::max<int64_t>(4, (cap / npix) & ~3ll));
-    if (g_tune.phase_kcap > 0) kcap = std::min(kcap, g_tune.phase_kcap);
+  const double first_bytes = (double)npix * K1 * (3 * sizeof(double) + (L.count ? 2 : 0));
+  // slots after the first phase: 24 B of radiance + 8 B of slot map each (+ 2 B of segments)
+  const int64_t cap =
+      std::min<int64_t>(0xFFFFFFFFll, slot_target(sc, 32 + (L.count ? 2 : 0), 1ll << kSlotTargetLog2, first_bytes));
+  if (npix * 4 > cap) return fail(RTX_ERR_NOMEM, "adaptive render: too many pixels for the device memory");
+  int32_t kcap = (int32_t)std::min<int64_t>(budget, std::max<int64_t>(4, (cap / npix) & ~3ll));
+  if (g_tune.phase_kcap > 0) kcap = std::min(kcap, g_tune.phase_kcap);
+  {
     const int64_t slots = npix * (int64_t)kcap;
     if ((rc = w.lbuf.reserve(slots * 3 * sizeof(double)))) return rc;
     if (L.count && (rc = w.segs.reserve(slots * sizeof(uint16_t)))) return rc;
@@ -893,17 +763,10 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     if ((rc = w.total_h.reserve(2 * sizeof(unsigned long long)))) return rc;
     if (!w.ev) HIPC(hipEventCreateWithFlags(&w.ev, hipEventDisableTiming));
   }
-  const double tile_margin = g_tune.tile_margin > 0 ? g_tune.tile_margin : kTileMargin;
-  const int32_t tile_kinc = g_tune.tile_kinc > 0 ? g_tune.tile_kinc : kTileKinc;
-  const double tile_mstep = g_tune.tile_mstep >= 0 ? g_tune.tile_mstep : kTileMarginStep;
-  const int32_t tile_tail = g_tune.tile_tail >= 0 ? g_tune.tile_tail : kTileTail;
-  const double tile_starve = g_tune.tile_starve >= 0 ? g_tune.tile_starve : kTileStarveGain;
-  const int32_t tile_split = g_tune.tile_split > 0 ? g_tune.tile_split : kTileSplit;
   unsigned long long* ctr = w.ctr.as<unsigned long long>();  // 8 region counters, then the slot count, ...
   const unsigned qb = (unsigned)((npix + kBlock - 1) / kBlock);
   // record + next batch sizes after phase g (its slots in Lph: the uniform first phase's, or the
-  // phase's slot map), then (phases) the next phase's prefix sum, slot map and (to the host)
-  // slot count
+  // phase's slot map), then the next phase's prefix sum, slot map and (to the host) slot count
   auto record = [&](int g, const double* Lph, int64_t active) -> int {
     AdaptPlan ap;
     ap.kcur = g == 1 ? nullptr : w.k[g & 1].as<uint32_t>();
@@ -911,11 +774,9 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ap.knext = w.k[(g + 1) & 1].as<uint32_t>();
     ap.kuni = K1, ap.sub_n = 1, ap.sub_j = 0;
     ap.min_spp = prm->min_spp, ap.budget = budget, ap.phase = g, ap.kcap = kcap;
-    // phases: a phase of at least ~phase_slots slots while pixels remain: once few pixels are
-    // left, their batches grow (up to the budget) instead of phases that are mostly launch
-    // tail; tiles: the smallest batch only (phase ends cost no drain)
-    ap.kmin = tiles ? tile_kinc
-                    : (int32_t)std::min<int64_t>(budget, (phase_slots + active - 1) / std::max<int64_t>(1, active));
+    // a phase of at least ~phase_slots slots while pixels remain: once few pixels are left,
+    // their batches grow (up to the budget) instead of phases that are mostly launch tail
+    ap.kmin = (int32_t)std::min<int64_t>(budget, (phase_slots + active - 1) / std::max<int64_t>(1, active));
     ap.rel = prm->rel_threshold;
     ap.margin_step = g_tune.phase_mstep >= 0 ? g_tune.phase_mstep : kAdaptMarginStep;
     ap.segs = !L.count ? nullptr : g == 1 ? sc->segs1.as<uint16_t>() : w.segs.as<uint16_t>();
@@ -925,7 +786,6 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     // (ap.next_active was zeroed with the phase's slot counter block, k_slot_block_init)
     hipLaunchKernelGGL(k_adapt_record, dim3(qb), dim3(kBlock), 0, s, px, Lph, npix, npix, ap);
     HIPC(hipGetLastError());
-    if (tiles) return RTX_OK;
     hipLaunchKernelGGL(k_adapt_floor, dim3(qb), dim3(kBlock), 0, s, ap.knext, npix, 1, 0, (const int32_t*)px.samples,
                        budget, kcap, phase_slots, (const unsigned long long*)ap.next_active);
     HIPC(hipGetLastError());
@@ -955,7 +815,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     int rc2;
     if (debug) HIPC(hipMemsetAsync(A.counters + 13, 0, 5 * sizeof(unsigned long long), s));  // (the timeline)
     if ((rc2 = mark(s))) return rc2;
-    if (L.count && Lg.map != 2 && (rc2 = set_segbuf(ctr, segs, s))) return rc2;
+    if (L.count && (rc2 = set_segbuf(ctr, segs, s))) return rc2;
     if ((rc2 = persist_m<false>(Lg, Ag, ctr))) return rc2;
     L.build = Lg.build;  // (the stats report the instantiation launched last)
     if ((rc2 = mark(s))) return rc2;
@@ -967,55 +827,19 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
       unsigned long long seg1 = 0;
       HIPC(hipEventElapsedTime(&ms, sc->ev[2], sc->ev[3]));
       HIPC(hipMemcpy(&seg1, A.counters, sizeof seg1, hipMemcpyDeviceToHost));
-      if (Lg.map == 2) {
-        uint32_t tc[9] = {};
-        HIPC(hipMemcpy(tc, w.tcount.p, sizeof tc, hipMemcpyDeviceToHost));
-        pixels = tc[8];
-      }
       unsigned long long tt[18] = {};
       HIPC(hipMemcpy(tt, A.counters, sizeof tt, hipMemcpyDeviceToHost));
       if (tt[13]) {  // counting build: the launch's timeline (us from the first block's start)
         const double t0 = (double)~tt[13];
         auto us = [&](unsigned long long v) { return ((double)v - t0) / 100.0; };
-        fprintf(stderr, "rtx adaptive: %s %d timeline: slots used up %.1f .. %.1f us, waves end %.1f .. %.1f us\n",
-                Lg.map == 2 ? "tiles after phase" : "phase", g, us(~tt[15]), us(tt[14]), us(~tt[17]), us(tt[16]));
+        fprintf(stderr, "rtx adaptive: phase %d timeline: slots used up %.1f .. %.1f us, waves end %.1f .. %.1f us\n",
+                g, us(~tt[15]), us(tt[14]), us(~tt[17]), us(tt[16]));
       }
-      fprintf(stderr, "rtx adaptive: %s %d: %lld pixels, launch %.3f ms, %llu segments (%.0f Mseg/s)\n",
-              Lg.map == 2 ? "tiles after phase" : "phase", g, (long long)pixels, ms, seg1 - seg0,
-              (double)(seg1 - seg0) / (ms * 1e3));
+      fprintf(stderr, "rtx adaptive: phase %d: %lld pixels, launch %.3f ms, %llu segments (%.0f Mseg/s)\n", g,
+              (long long)pixels, ms, seg1 - seg0, (double)(seg1 - seg0) / (ms * 1e3));
     }
     return RTX_OK;
   };
-  // the first pass inside the tile launch: tiles of every pixel in image order, each starting
-  // with min_spp samples per pixel (no uniform launch, no record kernel, no claim-order sort)
-  if (one_launch) {
-    RenderArgs Ag = A;
-    Ag.L = w.lbuf.as<double>(), Ag.conv = nullptr, Ag.K = 1, Ag.s0 = 0;
-    RegionCounts rcn{};
-    const int64_t nt = max_tiles;
-    for (int r = 0; r < 8; r++) {  // tile t's region: min(7, tp * t * 8 / npix)
-      auto first_tile = [&](int64_t q) { return std::min<int64_t>(nt, (q * npix + 8 * tp - 1) / (8 * tp)); };
-      rcn.c[r] = (uint32_t)((r == 7 ? nt : first_tile(r + 1)) - first_tile(r));
-    }
-    TileArgs ta{};
-    ta.act = nullptr, ta.order = nullptr, ta.rcount = w.tcount.as<uint32_t>(), ta.knext = nullptr;
-    ta.nact = w.tcount.as<uint32_t>() + 8;
-    ta.L = w.lbuf.as<double>();
-    ta.segs = L.count ? w.segs.as<uint16_t>() : nullptr;
-    ta.rec_segs = A.counters + 9;
-    ta.px = px, ta.npix = npix;
-    ta.kcap = kcap, ta.min_spp = prm->min_spp, ta.budget = budget, ta.kinc = tile_kinc;
-    ta.max_blocks = (int32_t)max_blocks, ta.k1 = std::min(K1, kcap);  // (a batch never exceeds kcap)
-    ta.tp = tp, ta.nt = ntl, ta.tail_px = tile_tail, ta.split = tile_split;
-    ta.rel = prm->rel_threshold, ta.margin = tile_margin, ta.margin_step = tile_mstep, ta.starve_gain = tile_starve;
-    hipLaunchKernelGGL(k_tile_setup, dim3(1), dim3(1), 0, s, ta, w.targs.as<TileArgs>(), ctr, rcn, (uint32_t)npix,
-                       w.tcount.as<uint32_t>());
-    HIPC(hipGetLastError());
-    Launch Lg = L;
-    Lg.map = 2;
-    Lg.max_grid = (int)max_blocks;
-    return launch(1, Lg, Ag, nullptr, npix);
-  }
   // phase 1: min_spp samples of every pixel, one uniform launch over the whole render (the
   // scene's radiance buffer)
   if ((rc = sc->lbuf.reserve((size_t)npix * K1 * 3 * sizeof(double)))) return rc;
@@ -1035,47 +859,8 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   RenderArgs Ag = A;
   Ag.L = w.lbuf.as<double>();
   Ag.conv = nullptr;    // only pixels still sampling have slots
-  Ag.K = 1, Ag.s0 = 0;  // (unused: slots from the phase's slot map / the tiles)
+  Ag.K = 1, Ag.s0 = 0;  // (unused: slots from the phase's slot map)
   Launch Lg = L;
-  if (tiles) {
-    // the claim order: active pixels (knext != 0) compacted in image order, tiles keyed by
-    // (region, work descending), sorted; then the one launch of every further phase
-    uint32_t* knext = w.k[0].as<uint32_t>();  // record(1) wrote the first batches here
-    uint32_t* flag = w.k[1].as<uint32_t>();
-    uint32_t* tc = w.tcount.as<uint32_t>();
-    hipLaunchKernelGGL(k_tile_flags, dim3(qb), dim3(kBlock), 0, s, (const uint32_t*)knext, npix, flag);
-    HIPC(hipGetLastError());
-    HIPC(rtxscan::exclusive_scan_u32(flag, w.off.as<uint32_t>(), npix, w.scan_tmp.p, w.scan_tmp.n, s));
-    HIPC(hipMemsetAsync(tc, 0, 16 * sizeof(uint32_t), s));
-    hipLaunchKernelGGL(k_tile_compact, dim3(qb), dim3(kBlock), 0, s, (const uint32_t*)flag,
-                       (const uint32_t*)w.off.as<uint32_t>(), npix, w.act.as<uint32_t>(), tc + 8);
-    HIPC(hipGetLastError());
-    const unsigned tb = (unsigned)std::max<int64_t>(1, (max_tiles + kBlock - 1) / kBlock);
-    hipLaunchKernelGGL(k_tile_keys, dim3(tb), dim3(kBlock), 0, s, (const uint32_t*)w.act.as<uint32_t>(),
-                       (const uint32_t*)(tc + 8), (const uint32_t*)knext, npix, max_tiles, (int32_t)tp,
-                       w.tkeys[0].as<uint32_t>(),
-                       w.tvals[0].as<uint32_t>(), tc);
-    HIPC(hipGetLastError());
-    HIPC(rtxscan::sort_pairs_u32(w.tkeys[0].as<uint32_t>(), w.tkeys[1].as<uint32_t>(), w.tvals[0].as<uint32_t>(),
-                                 w.tvals[1].as<uint32_t>(), max_tiles, w.sort_tmp.p, w.sort_tmp.n, s));
-    TileArgs ta{};
-    ta.act = w.act.as<uint32_t>(), ta.order = w.tvals[1].as<uint32_t>(), ta.rcount = tc, ta.knext = knext;
-    ta.nact = tc + 8;
-    ta.L = w.lbuf.as<double>();
-    ta.segs = L.count ? w.segs.as<uint16_t>() : nullptr;
-    ta.rec_segs = A.counters + 9;
-    ta.px = px, ta.npix = npix;
-    ta.kcap = kcap, ta.min_spp = prm->min_spp, ta.budget = budget, ta.kinc = tile_kinc;
-    ta.max_blocks = (int32_t)max_blocks, ta.k1 = K1;
-    ta.tp = tp, ta.nt = ntl, ta.tail_px = tile_tail, ta.split = tile_split;
-    ta.rel = prm->rel_threshold, ta.margin = tile_margin, ta.margin_step = tile_mstep, ta.starve_gain = tile_starve;
-    hipLaunchKernelGGL(k_tile_setup, dim3(1), dim3(1), 0, s, ta, w.targs.as<TileArgs>(), ctr, RegionCounts{},
-                       (uint32_t)npix, w.tcount.as<uint32_t>());
-    HIPC(hipGetLastError());
-    Lg.map = 2;
-    Lg.max_grid = (int)max_blocks;
-    return launch(2, Lg, Ag, nullptr, 0);
-  }
   Lg.map = 1;
   for (int g = 2;; g++) {
     // this phase's slot count, computed at the end of the previous one
@@ -1254,13 +1039,7 @@ int rtx_scene_create(int device, const rtx_scene_desc* d, rtx_scene** out) {
       sc->stack_fast = need < 0 ? -1 : (need <= 32 ? 32 : (need <= 64 ? 64 : -1));
       sc->fast_need = need;
       sc->n_f4 = f4.size();
-#if RTX_QNODE
-      std::vector<QNode> qn;
-      if (!quantise_f4(f4, qn)) sc->stack_fast = -1;  // (no fast path: the parity walk serves the scene)
-      if (sc->stack_fast > 0 && (rc = upload(sc->fnodes, qn.data(), qn.size(), s))) return rc;
-#else
       if (sc->stack_fast > 0 && (rc = upload(sc->fnodes, f4.data(), f4.size(), s))) return rc;
-#endif
       sc->fast_ok = sc->stack_fast > 0;
     }
   }
@@ -1562,39 +1341,6 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   uint64_t hot_launches = 0;
   if (timed) HIPC(hipEventRecord(sc->ev[0], s));
   const int pix_blocks = (int)((npix + kBlock - 1) / kBlock);
-  // frame parts (see the loop): fixed-spp persistent frames of one sample group with a band sink
-  int split_parts = 1;
-  int64_t split_pb[kMaxFrameParts + 1] = {0};
-  int split_bands[kMaxFrameParts] = {0};
-  bool split_done = false;
-  if (banded && !phased && prm->mode != RTX_MODE_WAVEFRONT && K >= budget) {
-    const int parts = std::min(kMaxFrameParts, g_frame_parts > 0 ? g_frame_parts : kFrameParts);
-    const double last = g_frame_last_share > 0 ? g_frame_last_share : kFrameLastShare;
-    // part edges: whole rows of the pixel map's layout and whole bands of the sink
-    const int64_t row = map.stripes ? (int64_t)map.srows * map.W : (int64_t)map.w;
-    const int64_t unit = std::lcm<int64_t>(row, std::max<int64_t>(1, sink->align));
-    const int64_t units = npix / unit;  // (a partial unit at the end joins the last part)
-    if (parts > 1 && units >= parts) {
-      split_parts = parts;
-      int64_t prev = 0;  // (in units; every part at least one)
-      for (int q = 1; q < parts; q++) {
-        const double f = (1.0 - last) * q / (parts - 1);
-        prev = std::max<int64_t>(prev + 1, std::min<int64_t>(units - (parts - q), (int64_t)(f * units + 0.5)));
-        split_pb[q] = prev * unit;
-      }
-      split_pb[parts] = npix;
-      for (int q = 0; q < parts; q++)  // (never reached: the host check before any launch)
-        if (!(split_pb[q] < split_pb[q + 1] && split_pb[q + 1] <= npix)) return fail(RTX_ERR_INVALID, "bad frame parts");
-      for (int q = 0; q < parts; q++)  // bands: the last part's the finest (its copy ends the frame)
-        split_bands[q] = q + 1 < parts ? std::max(1, kBands / 2) : kBands;
-    }
-  }
-  if (split_parts > 1)
-    while (sc->band_ev.size() < (size_t)(kBands * kMaxFrameParts + 1)) {
-      hipEvent_t e = nullptr;
-      HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      sc->band_ev.push_back(e);
-    }
   const int wf_grid = std::max(1, std::min<int>(sc->cus * 16, (int)((nslots + kBlock - 1) / kBlock)));
   if (phased) {
     if ((rc = render_adaptive(sc, L, A, prm, px, budget, s, [&](hipStream_t st) -> int {
@@ -1639,60 +1385,6 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
         HIPC(hipGetLastError());
         hot_launches++;
       }
-    } else if (split_parts > 1) {
-      // Frame parts: part q traces pixels [pb[q], pb[q + 1]) with its own slot counters, the
-      // parts after the first on part_stream, so their workgroups take the CUs an earlier
-      // part's drain frees.  Each part's accumulate (its bands and their copies) follows its own
-      // launch on its own stream and runs in the next part's drain; only the last, smallest
-      // part's accumulate follows the frame's last launch.  Kernel boundaries order every
-      // radiance record before its sum; the results are the one-launch frame's bit for bit.
-      if (!sc->part_stream) HIPC(hipStreamCreateWithFlags(&sc->part_stream, hipStreamNonBlocking));
-      while (sc->part_ev.size() < (size_t)(kMaxFrameParts + 3)) {
-        hipEvent_t e = nullptr;
-        HIPC(hipEventCreate(&e));
-        sc->part_ev.push_back(e);
-      }
-      for (int q = 0; q < split_parts; q++)
-        HIPC(hipMemsetAsync(next_slot + q * kSlotBlockWords, 0, 8 * 16 * sizeof(unsigned long long), s));
-      HIPC(hipEventRecord(sc->part_ev[0], s));  // setup done (and the frame's hot start)
-      HIPC(hipStreamWaitEvent(sc->part_stream, sc->part_ev[0], 0));
-      int band0 = 0;
-      for (int q = 0; q < split_parts; q++) {
-        hipStream_t sq = q == 0 ? s : sc->part_stream;
-        RenderArgs Aq = A;
-        Aq.npix = split_pb[q + 1] - split_pb[q];
-        Aq.L = A.L + 3 * split_pb[q] * (int64_t)Kc;
-        Aq.map = sub_map(map, split_pb[q]);
-        Launch Lq = L;
-        Lq.s = sq;
-        rc = prm->mode == RTX_MODE_MEGAKERNEL ? persist_m<true>(Lq, Aq, next_slot + q * kSlotBlockWords)
-                                              : persist_m<false>(Lq, Aq, next_slot + q * kSlotBlockWords);
-        if (rc) return rc;
-        L.build = Lq.build;
-        HIPC(hipEventRecord(sc->part_ev[1 + q], sq));  // part q's end
-        const AccOut out{d_rgb, d_spp, prm->mode == RTX_MODE_MEGAKERNEL ? 1 : 0, prm->spp};
-        const int64_t align = std::max<int64_t>(1, sink->align);
-        const int64_t u0 = split_pb[q] / align, u1 = (split_pb[q + 1] + align - 1) / align;
-        const int nb = split_bands[q];
-        for (int b = 0; b < nb; b++) {
-          const int64_t q0 = std::min<int64_t>(npix, (u0 + (u1 - u0) * b / nb) * align);
-          const int64_t q1 = std::min<int64_t>(npix, (u0 + (u1 - u0) * (b + 1) / nb) * align);
-          if (q1 <= q0) continue;
-          hipLaunchKernelGGL(k_accumulate_sum, dim3((unsigned)((q1 - q0 + kAccPix - 1) / kAccPix)), dim3(kAccWave), 0,
-                             sq, px, A.L, npix, Kc, q0, q1, 1, out);
-          HIPC(hipGetLastError());
-          HIPC(hipEventRecord(sc->band_ev[band0 + b], sq));
-          HIPC(hipStreamWaitEvent(sc->copy_stream, sc->band_ev[band0 + b], 0));
-          if ((rc = sink->copy(sink->ctx, q0, q1, sc->copy_stream))) return rc;
-        }
-        band0 += nb;
-      }
-      HIPC(hipEventRecord(sc->part_ev[kMaxFrameParts + 2], sc->part_stream));  // the part stream's work done
-      HIPC(hipStreamWaitEvent(s, sc->part_ev[kMaxFrameParts + 2], 0));
-      hot_launches++;
-      split_done = true;
-      resolved = true;
-      continue;
     } else {
       HIPC(hipMemsetAsync(next_slot, 0, 8 * 16 * sizeof(unsigned long long), s));
       if ((rc = hot_begin())) return rc;
@@ -1765,13 +1457,6 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
       float hms = 0;
       HIPC(hipEventElapsedTime(&hms, sc->evpool[e], sc->evpool[e + 1]));
       hot_ms += hms;
-    }
-    // a frame in parts: its hot time is the union of the parts' launches (they overlap), from
-    // the first one's start to the last one's end
-    for (int q = 0; split_done && q < split_parts; q++) {
-      float hms = 0;
-      HIPC(hipEventElapsedTime(&hms, sc->part_ev[0], sc->part_ev[1 + q]));
-      if (q == 0 || hms > hot_ms) hot_ms = hms;
     }
     unsigned long long h[18];
     std::memcpy(h, sc->counters_h.p, sizeof h);
@@ -2130,50 +1815,35 @@ extern "C" int rtx_internal_check_sincos(int device, int64_t n, uint64_t seed, i
   return RTX_OK;
 }
 
-// Test / tuning hook (not in rtx.h): overrides of the adaptive schedules' constants for the
-// renders that follow in this process (0 restores a default): the tile schedule's largest and
-// smallest batch of a pixel and its batch margin; the phase schedule's smallest phase and
-// largest batch.  Results never depend on them, only the amount of work and the number of
-// phases do (tests/test_gpu_timed.py runs the full budgets through forced small workspaces).
-extern "C" int rtx_internal_adapt_tune(int32_t tile_kcap, int32_t tile_kinc, double tile_margin, int64_t phase_slots,
-                                       int32_t phase_kcap, int32_t tile_first_pass, int32_t tile_tp, int32_t tile_nt,
-                                       double tile_mstep, int32_t tile_tail, double tile_starve, int32_t tile_split,
-                                       int32_t first_map, double phase_mstep) {
-  if (tile_kcap < 0 || tile_kinc < 0 || !(tile_margin >= 0) || phase_slots < 0 || phase_kcap < 0 ||
-      tile_first_pass < 0 || tile_first_pass > 2 || tile_tp < 0 || tile_tp > kTileTP || tile_nt < 0 ||
-      tile_nt > kTileNT || tile_split < 0 || first_map > 1)
-    return fail(RTX_ERR_INVALID, "bad tuning value");
-  g_tune = AdaptTune{tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap, tile_first_pass, tile_tp, tile_nt,
-                     tile_mstep, tile_tail, tile_starve, tile_split, first_map, phase_mstep};
-  return RTX_OK;
-}
-
-// Test / tuning hook (not in rtx.h): the frame parts of fixed-spp frames (parts: 1 one launch,
-// up to kMaxFrameParts; last_share: the last part's share of the pixels; 0 restores a default).
-// Results never depend on them.
-extern "C" int rtx_internal_frame_parts(int32_t parts, double last_share) {
-  if (parts < 0 || parts > kMaxFrameParts || !(last_share >= 0.0 && last_share < 1.0))
-    return fail(RTX_ERR_INVALID, "bad frame parts");
-  g_frame_parts = parts, g_frame_last_share = last_share;
+// Test / tuning hook (not in rtx.h): overrides of the adaptive phases' constants for the
+// renders that follow in this process (0 / negative restores a default): the smallest phase,
+// the largest batch of a pixel, the first pass's kernel (1 the phase kernel, 0 the uniform-group
+// one) and the batch margin's growth per phase.  Results never depend on them, only the amount
+// of work and the number of phases do (tests/test_gpu_timed.py runs the full budgets through
+// forced small workspaces).
+extern "C" int rtx_internal_adapt_tune(int64_t phase_slots, int32_t phase_kcap, int32_t first_map, double phase_mstep) {
+  if (phase_slots < 0 || phase_kcap < 0 || first_map > 1) return fail(RTX_ERR_INVALID, "bad tuning value");
+  g_tune = AdaptTune{phase_slots, phase_kcap, first_map, phase_mstep};
   return RTX_OK;
 }
 
 // Test hook (not in rtx.h): the persistent kernel's LDS layout (persist_lds) for a traversal
 // stack of stack_slots entries per lane and a schedule (park: 0 plain, 1 PARK with the
-// leaf-step walk, 2 PARK with the speculative walk; + 4: the adaptive tile schedule's launch,
-// + 8: an adaptive phase launch, with its block-shared slot chunks):
-// out[0..5] = byte offsets of the stack, throughput, hit point, leaf queue, tile descriptors and
-// the block's LDS size; out[6..9] = the first four regions' bytes per lane (entries x element
-// size; they are lane-interleaved with stride kBlock), out[10] = the block-wide region's bytes
-// (tile descriptors or chunk words).  tests/test_capi_exports.py checks that the regions are disjoint and
+// leaf-step walk, 2 PARK with the speculative walk; + 8: an adaptive phase launch, with its
+// block-shared slot chunks):
+// out[0..5] = byte offsets of the stack, throughput, hit point, leaf queue, block-wide region
+// and the block's LDS size; out[6..9] = the first four regions' bytes per lane (entries x
+// element size; they are lane-interleaved with stride kBlock), out[10] = the block-wide region's
+// bytes (the chunk words).  tests/test_capi_exports.py checks that the regions are disjoint and
 // inside the block's LDS for every stack size the host can choose.
 extern "C" int rtx_internal_lds_layout(int stack_slots, int park, uint32_t* out) {
-  const int block_kind = (park & 4) ? 2 : (park & 8) ? 1 : 0;
+  const int block_kind = (park & 8) ? 1 : 0;
+  if ((park & ~11) || stack_slots < 1 || stack_slots > 65 || (park & 3) > 2 || !out)
+    return fail(RTX_ERR_INVALID, "bad argument");
   park &= 3;
-  if (stack_slots < 1 || stack_slots > 65 || park < 0 || park > 2 || !out) return fail(RTX_ERR_INVALID, "bad argument");
   const bool spec = spec_walk(park, true, false);
   const PersistLds l = persist_lds(stack_slots, spec, block_kind);
-  const uint32_t v[11] = {l.stack, l.thr, l.hitp, l.leafq, l.tiles, l.end, (uint32_t)stack_slots * (spec ? 2u : 4u),
+  const uint32_t v[11] = {l.stack, l.thr, l.hitp, l.leafq, l.block, l.end, (uint32_t)stack_slots * (spec ? 2u : 4u),
                           24u, 24u, spec ? kLeafQueue * 4u : 0u, block_region_bytes(block_kind)};
   std::memcpy(out, v, sizeof v);
   return RTX_OK;

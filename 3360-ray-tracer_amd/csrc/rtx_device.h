@@ -12,30 +12,30 @@
 
 #include "rtx.h"
 
-// Per-translation-unit choices (the plain kernel's TU, rtx_capi.hip, takes the defaults; the
-// PARK TU, rtx_park.hip, sets its own before including this file).  Each was picked by A/B on
-// the scenes that run that TU's kernels (DESIGN.md ledger); every other alternative the
-// ledger records was measured and removed.
-#ifndef RTX_SINCOS_SMALL
-#define RTX_SINCOS_SMALL 1  // Lambertian cos/sin: 1 the restated small-argument forms, 0 the library's
-#endif
-#ifndef RTX_TRI_BRANCHLESS
-#define RTX_TRI_BRANCHLESS 0  // kind-specialised walks: the triangle test without early exits
-#endif
-#ifndef RTX_EARLY_TEX
-#define RTX_EARLY_TEX 1  // textured builds: a Lambertian's albedo texture looked up before the sampling
-#endif
-#ifndef RTX_LEAF_STEP
-#define RTX_LEAF_STEP 0  // lean walk: at most one leaf test per lane and loop iteration (trace4_run_step)
-#endif
-#ifndef RTX_SHARED_CHUNKS0
-#define RTX_SHARED_CHUNKS0 0  // uniform-group launches (MAP 0) with the block-shared slot chunks too (A/B)
-#endif
-#ifndef RTX_CAM_KARG
-#define RTX_CAM_KARG 0  // Lambertian texture-free builds: the camera read from the argument segment at refill (A/B)
+// Per-translation-unit choices.  rtx_park.hip, which compiles the PARK instantiations of
+// k_persistent and nothing else, defines RTX_PARK_TU 1 before including this file; every
+// other translation unit (rtx_capi.hip: the plain kernel, the frame kernels) takes the plain
+// kernel's choices.  Each was picked by A/B on the scenes that run that TU's kernels (DESIGN.md
+// ledger); register allocation decides which is best per kernel.  k_persistent asserts that
+// its PARK instantiations come from the PARK TU only.
+#ifndef RTX_PARK_TU
+#define RTX_PARK_TU 0
 #endif
 
 namespace rtxd {
+
+// Lambertian cos/sin: the restated small-argument forms (plain TU; with them the bunny's PARK
+// build spills, 0 -> 56 B per lane), else the library's cos() / sin()
+constexpr bool kSincosSmall = !RTX_PARK_TU;
+// kind-specialised walks: the triangle test without early exits (PARK TU: bunny +3.8 %; the
+// plain kernel's builds are slower with it)
+constexpr bool kTriBranchless = RTX_PARK_TU;
+// textured builds: a Lambertian's albedo texture looked up before the sampling (plain TU; the
+// early lookup makes the generic PARK build spill more, 80 -> 128 B per lane)
+constexpr bool kEarlyTex = !RTX_PARK_TU;
+// lean walk: at most one leaf test per lane and loop iteration (trace4_run_step; PARK TU: bunny
+// +2.8 %; the plain kernel's sphere-tree builds are slower with it)
+constexpr bool kLeafStep = RTX_PARK_TU;
 
 constexpr double kPi = 3.14159265358979323846;
 constexpr double kInf = __builtin_inf();
@@ -163,10 +163,9 @@ __device__ __forceinline__ V3 random_in_unit_disk(Rng& g) {  // math_utils.h:83-
 // Lambertian angle 2*pi*r1 < 2*pi never takes, is not compiled in: its registers made the
 // shading spill.  -ffp-contract=off keeps every product and sum separately rounded, as in
 // the library; fma() is the library's fma.
-//   RTX_SINCOS_SMALL 1: cos and sin each from its own small-argument reduction (fewest live
+//   kSincosSmall: cos and sin each from its own small-argument reduction (fewest live
 //   registers: the plain kernel's texture-free builds lose their last spills, A/B r02
-//   `ab_sincos2_*`; one shared reduction spilled more); 0: the library's cos() and sin().
-// Register allocation decides which is best per kernel, so the PARK TU picks its own value.
+//   `ab_sincos2_*`; one shared reduction spilled more); else the library's cos() and sin().
 __device__ __forceinline__ void sincos_small(double x, double& sn, double& cs) {
   // reduction: x = q * pi/2 + (hi + lo)
   const double q = rint(x * 0x1.45f306dc9c883p-1);
@@ -207,15 +206,15 @@ __device__ __forceinline__ void sincos_small(double x, double& sn, double& cs) {
   sn = quad > 1 ? -s0 : s0;
 }
 __device__ __forceinline__ void cos_sin(double phi, double& c, double& s) {
-#if RTX_SINCOS_SMALL
-  double t;
-  sincos_small(phi, t, c);
-  asm volatile("" : "+v"(c));
-  asm volatile("" : "+v"(phi));
-  sincos_small(phi, s, t);
-#else
-  c = cos(phi), s = sin(phi);
-#endif
+  if constexpr (kSincosSmall) {
+    double t;
+    sincos_small(phi, t, c);
+    asm volatile("" : "+v"(c));
+    asm volatile("" : "+v"(phi));
+    sincos_small(phi, s, t);
+  } else {
+    c = cos(phi), s = sin(phi);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -240,27 +239,7 @@ struct F4Node {
 };
 static_assert(sizeof(F4Node) == 128, "F4Node must be two 64-byte lines");
 
-// RTX_QNODE (A/B): the same 4-wide nodes quantised into one 64-byte line.  Per axis a, the
-// node's f32 origin o[a] and a power-of-two step s[a]; per child and axis, the entry and exit
-// planes as bytes q: plane = fma(q, s, o), an exact product rounded once.  The host
-// (quantise_f4, rtx_capi.hip) picks each q so that the decoded plane lies outside the F4Node's
-// outward-rounded f32 plane (checked with the same fmaf), so a decoded box contains the f32
-// box and the slab test on it stays conservative with the same argument as on the f32 box.
-// Empty slots: lo bytes 255, hi bytes 0 (an inverted box).
-struct QNode {
-  float o[3], s[3];
-  int32_t child[4];
-  uint32_t qlo[3], qhi[3];  // axis a: byte c = child slot c's plane
-};
-static_assert(sizeof(QNode) == 64, "QNode must be one 64-byte line");
-#ifndef RTX_QNODE
-#define RTX_QNODE 0
-#endif
-#if RTX_QNODE
-typedef QNode FastNode;
-#else
 typedef F4Node FastNode;
-#endif
 
 struct DScene {
   const rtx_bvh_node* nodes;  // parity layout, reference pre-order
@@ -461,7 +440,7 @@ __device__ __forceinline__ bool prim_t_rec(const PrimRec& R, V3 o, V3 d, double 
   mat_out = R.mat;
   const PrimRec* P = &R;
   const int kind = KIND >= 0 ? KIND : P->kind;
-  if (RTX_TRI_BRANCHLESS && KIND >= 0 && kind == RTX_PRIM_TRIANGLE) {
+  if (kTriBranchless && KIND >= 0 && kind == RTX_PRIM_TRIANGLE) {
     // the same operations without the early exits: every value is computed and the four
     // rejections are combined at the end (a wave's few active leaf lanes rarely all take
     // the same early exit, so the branches only add mask bookkeeping)
@@ -773,9 +752,6 @@ __device__ __forceinline__ FRay4L make_fray4l(V3 o, V3 d) {
   fray4_axis_signed(o.x, d.x, 0, b.ix, b.nlx, b.nhx, b.ox);
   fray4_axis_signed(o.y, d.y, 1, b.iy, b.nly, b.nhy, b.oy);
   fray4_axis_signed(o.z, d.z, 2, b.iz, b.nlz, b.nhz, b.oz);
-#if RTX_QNODE  // entry-plane word of axis a: qlo[a] (byte 40 + 4a) for inv >= 0, else qhi[a] (52 + 4a)
-  b.ox = b.ox & 16u ? 52u : 40u, b.oy = b.oy & 16u ? 56u : 44u, b.oz = b.oz & 16u ? 60u : 48u;
-#endif
   constexpr float lo = 0.99999f, hi = 1.00001f;
   FRay4L r;
   r.iex = b.ix * lo, r.iey = b.iy * lo, r.iez = b.iz * lo;
@@ -830,38 +806,6 @@ __device__ __forceinline__ void trav_globals(const DScene& S, V3 o, V3 d, double
 // Pieces of a lean BVH4 node visit shared by trace4_run and trace4_run_step.
 // The slab tests of node `node`'s four slots: entry distances of the internal children entered
 // (+inf otherwise) in tt, the child words in cc; returns the mask of leaf slots entered.
-#if RTX_QNODE
-__device__ __forceinline__ uint32_t visit_slabs(const char* __restrict__ nbase, uint32_t node, const FRay4L& r,
-                                                float tmax_x, float (&tt)[4], int32_t (&cc)[4]) {
-  const uint32_t noff = node << 6;  // sizeof(QNode) == 64
-  const uint4 w0 = *(const uint4*)(nbase + noff), w1 = *(const uint4*)(nbase + (noff + 16u));
-  const uint4 w2 = *(const uint4*)(nbase + (noff + 32u)), w3 = *(const uint4*)(nbase + (noff + 48u));
-  const uint32_t wv[16] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w, w2.x, w2.y, w2.z, w2.w, w3.x, w3.y, w3.z, w3.w};
-  const float ox = __uint_as_float(wv[0]), oy = __uint_as_float(wv[1]), oz = __uint_as_float(wv[2]);
-  const float sx = __uint_as_float(wv[3]), sy = __uint_as_float(wv[4]), sz = __uint_as_float(wv[5]);
-  cc[0] = (int32_t)wv[6], cc[1] = (int32_t)wv[7], cc[2] = (int32_t)wv[8], cc[3] = (int32_t)wv[9];
-  // entry / exit plane words by the ray's signs (qlo at words 10..12, qhi at 13..15)
-  const uint32_t ex = r.ox == 40u ? wv[10] : wv[13], fx = r.ox == 40u ? wv[13] : wv[10];
-  const uint32_t ey = r.oy == 44u ? wv[11] : wv[14], fy = r.oy == 44u ? wv[14] : wv[11];
-  const uint32_t ez = r.oz == 48u ? wv[12] : wv[15], fz = r.oz == 48u ? wv[15] : wv[12];
-  auto dq = [](uint32_t w, int c, float s, float o) {  // the decoded plane (exact product, one rounding)
-    const float q = (float)((w >> (8 * c)) & 0xFFu);  // (v_cvt_f32_ubyte<c>)
-    return fmaf(q, s, o);
-  };
-  uint32_t lmask = 0;
-#pragma unroll
-  for (int c = 0; c < 4; c++) {
-    const float tn = fmaxf(fmaxf(fmaf(dq(ex, c, sx, ox), r.iex, r.nex), fmaf(dq(ey, c, sy, oy), r.iey, r.ney)),
-                           fmaxf(fmaf(dq(ez, c, sz, oz), r.iez, r.nez), 0.0f));
-    const float tf = fminf(fminf(fmaf(dq(fx, c, sx, ox), r.ixx, r.nxx), fmaf(dq(fy, c, sy, oy), r.ixy, r.nxy)),
-                           fminf(fmaf(dq(fz, c, sz, oz), r.ixz, r.nxz), tmax_x));
-    const bool hit = tn <= tf;
-    lmask |= (hit && cc[c] < 0) ? (1u << c) : 0u;
-    tt[c] = (hit && cc[c] >= 0) ? tn : __builtin_inff();
-  }
-  return lmask;
-}
-#else
 __device__ __forceinline__ uint32_t visit_slabs(const char* __restrict__ nbase, uint32_t node, const FRay4L& r,
                                                 float tmax_x, float (&tt)[4], int32_t (&cc)[4]) {
   const uint32_t noff = node << 7;  // sizeof(F4Node) == 128
@@ -883,7 +827,6 @@ __device__ __forceinline__ uint32_t visit_slabs(const char* __restrict__ nbase, 
   }
   return lmask;
 }
-#endif
 // The primitive of leaf slot c (its child word holds ~index)
 __device__ __forceinline__ uint32_t leaf_prim(const int32_t (&cc)[4], int c) {
   const int32_t c01 = (c & 1) ? cc[1] : cc[0], c23 = (c & 1) ? cc[3] : cc[2];
@@ -1068,7 +1011,7 @@ __device__ __forceinline__ bool trace4_run_spec(const DScene& S, V3 o, V3 d, dou
 template <int STACK, bool COUNT, int KIND = -1>
 __device__ __forceinline__ bool trace4_run(const DScene& S, V3 o, V3 d, double tmin, uint32_t* stk, int stride,
                                            Counters& cnt, TravState& ts, int park_at) {
-  if (RTX_LEAF_STEP) return trace4_run_step<STACK, COUNT, KIND>(S, o, d, tmin, stk, stride, cnt, ts, park_at);
+  if (kLeafStep) return trace4_run_step<STACK, COUNT, KIND>(S, o, d, tmin, stk, stride, cnt, ts, park_at);
   FRay4L r = make_fray4l(o, d);
   const char* __restrict__ nbase = (const char*)S.f4nodes;
   double closest = ts.closest, t;
@@ -1406,7 +1349,7 @@ __device__ __forceinline__ void shade_core(const DScene& S, int max_depth, Path&
   // direction sampling, so the hit point / u,v / lazy-uv sphere are dead during the sampling
   // (only the colour is kept); the same lookup, only earlier
   V3 ftex = v3(0, 0, 0);
-  if (RTX_EARLY_TEX && !NOTEX && !DEFER_F && isL) ftex = mat_tex_t<NOTEX>(S, m, rec);
+  if (kEarlyTex && !NOTEX && !DEFER_F && isL) ftex = mat_tex_t<NOTEX>(S, m, rec);
   double r1 = 0.0, r2 = 0.0;
   if (isL) r1 = g.next(), r2 = g.next();
   V3 ru = v3(0, 0, 0);
@@ -1478,7 +1421,7 @@ __device__ __forceinline__ void shade_core(const DScene& S, int max_depth, Path&
     const float cf = (float)dot(n, wi);
     const float pdf = (cf <= 0.0f) ? 0.0f : (float)((double)cf / kPi);
     if (DEFER_F) so.fsrc = 1;
-    else so.f = ((RTX_EARLY_TEX && !NOTEX) ? ftex : mat_tex_t<NOTEX>(S, m, rec)) / kPi;
+    else so.f = ((kEarlyTex && !NOTEX) ? ftex : mat_tex_t<NOTEX>(S, m, rec)) / kPi;
     if (pdf < 1e-6f) return;
     so.ct = fmaxf(0.0f, (float)dot(wi, n));
     so.pdf = pdf;

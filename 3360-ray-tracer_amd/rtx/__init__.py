@@ -19,11 +19,9 @@ RTX_SEAM_TMIN = float(np.float32(0.001))
 MODES = {"wavefront": 0, "persistent": 1, "megakernel": 2}
 PRECISIONS = {"parity": 0, "fast": 1}
 RTX_FLAG_COUNT, RTX_FLAG_PARK, RTX_FLAG_NO_PARK, RTX_FLAG_GENERIC, RTX_FLAG_LEAF_STEP = 1, 2, 4, 8, 16
-# adaptive persistent renders: one launch per phase (the default; ADAPT_PHASES names it) or the
-# tile schedule (ADAPT_TILES)
+# adaptive persistent renders: one launch per phase (the default; ADAPT_PHASES names it)
 RTX_FLAG_ADAPT_PHASES = 32
-RTX_FLAG_ADAPT_TILES = 64
-ADAPT_SCHEDULE_FLAGS = {None: 0, "phases": RTX_FLAG_ADAPT_PHASES, "tiles": RTX_FLAG_ADAPT_TILES}
+ADAPT_SCHEDULE_FLAGS = {None: 0, "phases": RTX_FLAG_ADAPT_PHASES}
 # "park": the PARK schedule with its default walk (speculative on trees of at most 65536 nodes);
 # "park_step": the PARK schedule with the leaf-step walk on every tree
 SCHEDULE_FLAGS = {None: 0, "auto": 0, "park": RTX_FLAG_PARK, "park_step": RTX_FLAG_PARK | RTX_FLAG_LEAF_STEP,
@@ -354,31 +352,17 @@ class DeviceScene:
         return st.as_dict() if stats else None
 
 
-def adapt_tune(tile_kcap=0, tile_kinc=0, tile_margin=0.0, phase_slots=0, phase_kcap=0, tile_first_pass=0,
-               tile_tp=0, tile_nt=0, tile_mstep=-1.0, tile_tail=-1, tile_starve=-1.0, tile_split=0, first_map=-1, phase_mstep=-1.0):
+def adapt_tune(phase_slots=0, phase_kcap=0, first_map=-1, phase_mstep=-1.0):
     """Test / tuning hook (rtx_internal_adapt_tune, not in rtx.h): overrides of the adaptive
-    schedules' constants for the renders that follow in this process; no argument (all 0)
-    restores the defaults.  Results never depend on them, only the work and the phases do.
-    tile_first_pass: 1 the first pass inside the tile launch, 2 a uniform launch of its own.
-    first_map: the uniform first pass on the phase kernel (1, block-shared chunks) or on the
-    uniform-group kernel (0).  phase_mstep: the phases' batch margin growth per phase."""
+    phases' constants for the renders that follow in this process; no argument restores the
+    defaults.  Results never depend on them, only the work and the phases do.  phase_slots: the
+    smallest phase while pixels remain; phase_kcap: the largest batch of one pixel; first_map:
+    the uniform first pass on the phase kernel (1, block-shared chunks) or on the uniform-group
+    kernel (0); phase_mstep: the batch margin's growth per phase."""
     f = lib().rtx_internal_adapt_tune
-    f.argtypes = [C.c_int32, C.c_int32, C.c_double, C.c_int64, C.c_int32, C.c_int32, C.c_int32, C.c_int32,
-                  C.c_double, C.c_int32, C.c_double, C.c_int32, C.c_int32, C.c_double]
+    f.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_double]
     f.restype = C.c_int
-    _check(f(tile_kcap, tile_kinc, tile_margin, phase_slots, phase_kcap, tile_first_pass, tile_tp, tile_nt,
-             tile_mstep, tile_tail, tile_starve, tile_split, first_map, phase_mstep), "rtx_internal_adapt_tune")
-
-
-def frame_parts(parts=0, last_share=0.0):
-    """Test / tuning hook (rtx_internal_frame_parts, not in rtx.h): fixed-spp frames of one
-    sample group with banded output (render_multi) are traced in `parts` launches over
-    consecutive pixel ranges, the last taking `last_share` of the pixels (1: one launch; 0 / 0.0
-    restore the defaults).  Results never depend on it."""
-    f = lib().rtx_internal_frame_parts
-    f.argtypes = [C.c_int32, C.c_double]
-    f.restype = C.c_int
-    _check(f(parts, last_share), "rtx_internal_frame_parts")
+    _check(f(phase_slots, phase_kcap, first_map, phase_mstep), "rtx_internal_adapt_tune")
 
 
 def render_multi(scenes, cam, spp, max_depth, seed=1234, adaptive=True, mode="persistent", precision="fast",

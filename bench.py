@@ -126,14 +126,10 @@ def main():
     ap.add_argument("--adaptive", action="store_true",
                     help="the reference's default sampling (wavefront.cc:42-43, 62-69, 125-127): per-pixel "
                          "adaptive, at least 16 samples, relative error 0.05f, up to the workload's spp")
-    ap.add_argument("--adapt-schedule", default="phases", choices=["tiles", "phases"],
-                    help="adaptive renders: one launch per phase (default) or, after the first pass, tiles in "
-                         "one launch (RTX_FLAG_ADAPT_TILES)")
-    ap.add_argument("--frame-parts", default="",
-                    help="fixed-spp frames in P launches over consecutive pixel ranges, the last with share F "
-                         "of the pixels: P or P:F (rtx.frame_parts; 1 = one launch; default: the library's)")
+    ap.add_argument("--adapt-schedule", default="phases", choices=["phases"],
+                    help="adaptive renders: one launch per phase (the library's schedule)")
     ap.add_argument("--adapt-tune", default="",
-                    help="tuning of the adaptive schedules (rtx.adapt_tune), e.g. tile_first_pass=1,tile_kcap=64 "
+                    help="tuning of the adaptive phases (rtx.adapt_tune), e.g. phase_slots=4194304,phase_mstep=0.5 "
                          "(never changes results, only the work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-adaptive-leg", action="store_true",
@@ -169,12 +165,9 @@ def main():
 
     import rtx
 
-    if args.frame_parts:
-        fp = args.frame_parts.split(":")
-        rtx.frame_parts(int(fp[0]), float(fp[1]) if len(fp) > 1 else 0.0)
     if args.adapt_tune:
         kv = dict(x.split("=") for x in args.adapt_tune.split(","))
-        rtx.adapt_tune(**{k: (float(v) if k in ("tile_margin", "tile_mstep", "tile_starve", "phase_mstep") else int(v)) for k, v in kv.items()})
+        rtx.adapt_tune(**{k: (float(v) if k in ("phase_mstep",) else int(v)) for k, v in kv.items()})
     workload = args.workload if args.workload != "auto" else ("c3_bunny" if world == 1 else "c4_bunny4k")
     scene_name, preset, width, spp, depth = WORKLOADS[workload]
     spp = args.spp or spp
@@ -400,7 +393,7 @@ def time_adaptive(torch, step, params, per_frame_fixed, fixed_value):
             "hot_launches_per_step": sts[-1]["hot_launches"],
             "rays_recorded_per_step": rec, "rays_traced_per_step": traced,
             "recorded_fraction_of_traced": rec / max(1.0, traced), "vs_fixed_spp_value": rec * n / el / 1e6 / fixed_value,
-            "schedule": "phases" if ap.flags & 32 else "tiles", "wave_rounds_idle_frac": idle,
+            "schedule": "phases", "wave_rounds_idle_frac": idle,
             "sampling": sampling_text(True), "_recorded_whole": rec}
 
 

@@ -41,12 +41,13 @@
 extern "C" {
 #endif
 
-#define RTX_ABI_VERSION 8  /* 2: rtx_stats.node_bytes; 3: rtx_stats.parked, RTX_FLAG_PARK / NO_PARK;
+#define RTX_ABI_VERSION 9  /* 2: rtx_stats.node_bytes; 3: rtx_stats.parked, RTX_FLAG_PARK / NO_PARK;
                               4: rtx_stats.build, RTX_FLAG_GENERIC, rtx_render_multi;
                               5: RTX_FLAG_LEAF_STEP, RTX_BUILD_SPECULATIVE; 6: rtx_stats.rays_recorded;
                               7: RTX_FLAG_ADAPT_PHASES (the adaptive tile schedule is the default),
                               rtx_stats.wave_rounds / wave_rounds_idle;
-                              8: RTX_FLAG_ADAPT_TILES (the phase schedule is the default again) */
+                              8: RTX_FLAG_ADAPT_TILES (the phase schedule is the default again);
+                              9: the tile schedule removed (flag bit 64 reserved, ignored) */
 
 enum {
   RTX_OK = 0,
@@ -213,12 +214,9 @@ enum {
      the leaf-step walk on every tree (same results) */
   RTX_FLAG_LEAF_STEP = 16,
   /* RTX_MODE_PERSISTENT adaptive renders (samples_per_group 0): one launch per phase over a
-     device-wide slot map (the default; this flag names it explicitly), or, with
-     RTX_FLAG_ADAPT_TILES, after the first pass the further passes in tiles of pixels inside
-     one launch, each tile recorded by the workgroup that traces it (same results; slower on
-     the bench scenes) */
-  RTX_FLAG_ADAPT_PHASES = 32,
-  RTX_FLAG_ADAPT_TILES = 64
+     device-wide slot map (the default; this flag names it explicitly) */
+  RTX_FLAG_ADAPT_PHASES = 32
+  /* 64: reserved (ABI <= 8: the adaptive tile schedule, removed; ignored) */
 };
 
 /* rtx_stats.build: which persistent-kernel build ran (the per-scene specialisations compile

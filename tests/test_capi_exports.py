@@ -59,7 +59,7 @@ def test_invalid_descriptors_rejected_before_launch(rtx_mod):
     assert rc == -1 and b"material out of range" in rtx_mod.lib().rtx_last_error()
 
 
-@pytest.mark.parametrize("park", [0, 1, 2, 4, 5, 6, 8, 9, 10])
+@pytest.mark.parametrize("park", [0, 1, 2, 8, 9, 10])
 def test_persistent_lds_regions_are_disjoint(rtx_mod, park):
     """The persistent kernel's LDS regions (traversal stacks, throughput, hit point, leaf queue)
     are each lane-interleaved with their own element size, so a byte shared by two regions
@@ -68,12 +68,11 @@ def test_persistent_lds_regions_are_disjoint(rtx_mod, park):
     cmp_spec6_fault.txt).  The layout the kernel and the launch share (persist_lds, exported as a
     host-only test hook) must keep every region inside the block's LDS and apart from the others,
     for every stack size the host can choose (the lean walk's exact bound + 1, up to 65), with and
-    without a block-wide region after them: the adaptive tile schedule's descriptors (park + 4)
-    or an adaptive phase launch's chunk words (park + 8)."""
+    without a block-wide region after them: an adaptive phase launch's chunk words (park + 8)."""
     f = rtx_mod.lib().rtx_internal_lds_layout
     f.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_uint32)]
     out = (C.c_uint32 * 11)()
-    spec, tiles = (park & 3) == 2, bool(park & 12)
+    spec, tiles = (park & 3) == 2, bool(park & 8)
     for slots in range(1, 66):
         assert f(slots, park, out) == 0
         stack, thr, hitp, leafq, tl, end, *per_lane = list(out)

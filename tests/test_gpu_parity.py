@@ -233,31 +233,20 @@ def test_adaptive_schedules_equal_uniform_groups(rtx_mod, dev_scenes, scene, pre
     # (the Cornell box is too noisy for any pixel to converge within 48 samples: every pixel
     # takes the whole budget through the growing batches)
     """Adaptive persistent renders predict each pixel's batches from its statistics: the phase
-    schedule (default: one launch per phase over a device-wide slot map, also with a forced
-    small workspace and phase floor) and the tile schedule (RTX_FLAG_ADAPT_TILES: after a
-    uniform first pass, one launch runs every further batch of tiles of pixels, each recorded
-    inside its workgroup; also with forced tiny batches: many phases per tile, largest batch 4 /
-    3 samples, smallest 1, margin 0.5).  Each gives the same pixels and sample counts,
-    bit for bit, as uniform groups of 4 samples over every pixel."""
+    schedule (one launch per phase over a device-wide slot map; also with a forced small
+    workspace and phase floor, and with the uniform first pass on either kernel) gives the same
+    pixels and sample counts, bit for bit, as uniform groups of 4 samples over every pixel."""
     cam = rtx_mod.camera(rtx_mod.camera_config(preset, width=w))
     d = dev_scenes(scene)
     kw = dict(seed=17, adaptive=True, mode="persistent", precision="fast", schedule=schedule)
     b, sb, stb = d.render(cam, spp, depth, samples_per_group=4, **kw)
     assert sb.min() >= min(16, spp) and sb.max() <= spp and ((sb < spp).any() or scene == "cornell")
-    runs = [("tiles", {}, {}), ("tiles_one_launch", dict(tile_first_pass=1), {}),
-            ("tiles_two_launches", dict(tile_first_pass=2), {}),
-            ("tiles_kcap4", dict(tile_kcap=4, tile_kinc=1, tile_margin=0.5), {}),
-            ("tiles_one_launch_kcap3", dict(tile_kcap=3, tile_kinc=2, tile_first_pass=1), {}),
-            ("tiles_no_split", dict(tile_split=1 << 30), {}), ("tiles_split1_tp1", dict(tile_split=1, tile_tp=1), {}),
-            ("tiles_tp8_nt2_tail", dict(tile_tp=8, tile_nt=2, tile_tail=3, tile_starve=1.0), {}),
-            ("tiles_kcap3", dict(tile_kcap=3, tile_kinc=2, tile_margin=2.0), {}),
-            ("phases", {}, {}),
-            ("phases_small", dict(phase_slots=1024, phase_kcap=8), {})]
+    runs = [("phases", {}), ("phases_small", dict(phase_slots=1024, phase_kcap=8)),
+            ("phases_first_uniform", dict(first_map=0)), ("phases_wide_margin", dict(phase_mstep=1.5))]
     try:
-        for name, tune, extra in runs:
+        for name, tune in runs:
             rtx_mod.adapt_tune(**tune)
-            a, sa, sta = d.render(cam, spp, depth, **kw, **extra,
-                                  adapt_schedule="tiles" if name.startswith("tiles") else None)
+            a, sa, sta = d.render(cam, spp, depth, **kw)
             assert np.array_equal(sa, sb), (name, np.nonzero(sa != sb)[0][:5])
             assert np.array_equal(a, b), name
             assert sta["rays_primary"] >= sa.sum(), name

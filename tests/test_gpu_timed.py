@@ -153,15 +153,11 @@ def test_adaptive_recorded_segments_equal_oracle(rtx_mod, orc, scenes, acase, ro
 
 # The configurations' own budgets through FORCED small workspaces (rtx_internal_adapt_tune):
 # the paths only a large frame at a large budget reaches on its own — a pixel's batches capped
-# (tile kcap, phase kcap / workspace), the phase floor few remaining pixels get, many phases —
-# compared with the oracle on sample counts, recorded segments and pixels.
+# (phase kcap / workspace), the phase floor few remaining pixels get, many phases — compared
+# with the oracle on sample counts, recorded segments and pixels.
 FULL_BUDGET_CASES = [(1, 200, 0.7), (3, 2048, 0.5)]  # bench case index, spp, band row (fraction of H)
-TUNES = {"tiles": ({}, False), "tiles_small": (dict(tile_kcap=8, tile_kinc=4, tile_margin=0.75), False),
-         "tiles_one": (dict(tile_kcap=1, tile_kinc=1), False), "phases": ({}, True),
-         "tiles_one_launch": (dict(tile_first_pass=1), False),
-         "tiles_one_launch_small": (dict(tile_first_pass=1, tile_kcap=8, tile_kinc=4), False),
-         "tiles_split2_kcap5": (dict(tile_split=2, tile_kcap=5, tile_tp=3, tile_nt=3), False),
-         "phases_small": (dict(phase_slots=4096, phase_kcap=8), True)}
+TUNES = {"phases": {}, "phases_small": dict(phase_slots=4096, phase_kcap=8),
+         "phases_kcap1": dict(phase_slots=64, phase_kcap=4), "phases_first_uniform": dict(first_map=0)}
 
 
 @pytest.mark.parametrize("tune", sorted(TUNES))
@@ -176,12 +172,11 @@ def test_adaptive_full_budget_small_workspace_matches_oracle(rtx_mod, orc, scene
     cam = rtx_mod.camera(rtx_mod.camera_config(preset, width=width))
     tile = (0, int(cam.image_height * yfrac), cam.image_width, 1)
     ref, ref_spp, ref_st = oracle(orc, path, preset, width, spp, depth, 616, tile, adaptive=1)
-    knobs, phases = TUNES[tune]
+    knobs = TUNES[tune]
     try:
         rtx_mod.adapt_tune(**knobs)
         rgb, sp, st = d.render(cam, spp, depth, seed=616, adaptive=True, mode="persistent", precision="fast",
-                               tile=tile, count=True, min_spp=ADAPTIVE_MIN, rel_threshold=ADAPTIVE_REL,
-                               adapt_schedule="phases" if phases else "tiles")
+                               tile=tile, count=True, min_spp=ADAPTIVE_MIN, rel_threshold=ADAPTIVE_REL)
     finally:
         rtx_mod.adapt_tune()
     ref_spp = ref_spp.ravel()
@@ -360,40 +355,6 @@ def test_render_multi_banded_output_one_device(rtx_mod, scenes):
                                                   precision=precision, out=out, samples_per_group=group)
             assert np.array_equal(out, full) and np.array_equal(sp, fsp), (mode, group)
             assert st["rays_total"] == fst["rays_total"]
-
-
-def test_frame_parts_are_bit_identical(rtx_mod, scenes):
-    """Fixed-spp frames of one sample group are traced in several launches over consecutive
-    pixel ranges (frame parts, the later ones on a second stream, each part's banded accumulate
-    and copies behind its own launch).  Any number of parts and any last share give the
-    one-launch frame bit for bit: every mode's sum, both persistent schedules, one and two
-    scenes (stripes) on the device, a frame height that is no multiple of the stripe height,
-    and counts of parts the frame cannot hold (one launch then)."""
-    import torch
-
-    try:
-        for name, cfg, width, depth in (("final", "c2_final", 76, 50), ("bunny", "c3_bunny", 64, 20)):
-            path, d = scenes(name)
-            cam = rtx_mod.camera(rtx_mod.camera_config(cfg, width=width))
-            npix = cam.image_width * cam.image_height
-            other = rtx_mod.DeviceScene(rtx_mod.HostScene.load(path))
-            for mode, precision, schedule in (("persistent", "fast", "park"), ("persistent", "fast", "plain"),
-                                              ("persistent", "parity", None), ("megakernel", "fast", None)):
-                rtx_mod.frame_parts(1)
-                ref, rsp, rst, _ = rtx_mod.render_multi([d], cam, 4, depth, seed=33, adaptive=False, mode=mode,
-                                                        precision=precision, schedule=schedule)
-                for parts, share in ((2, 0.25), (2, 0.6), (3, 0.1), (4, 0.3), (4, 0.95)):
-                    rtx_mod.frame_parts(parts, share)
-                    for group in ([d], [d, other]):
-                        pinned = torch.full((npix, 3), -1.0, dtype=torch.float64).pin_memory()
-                        out = pinned.numpy()
-                        rgb, sp, st, _ = rtx_mod.render_multi(group, cam, 4, depth, seed=33, adaptive=False, mode=mode,
-                                                              precision=precision, schedule=schedule, out=out)
-                        key = (name, mode, precision, schedule, parts, share, len(group))
-                        assert np.array_equal(out, ref) and np.array_equal(sp, rsp), key
-                        assert st["rays_total"] == rst["rays_total"], key
-    finally:
-        rtx_mod.frame_parts()
 
 
 def test_render_multi_rejects_bad_arguments(rtx_mod, scenes):
