@@ -18,11 +18,11 @@ Other workloads: --workload c2_final | c5_mixed | c1_three | c4_bunny4k | c3_bun
 Prints ONE JSON line (rank 0).  `roofline` prices the dominant kernel (k_persistent) against
 its binding resource, VALU issue: useful lane-operations per second (VALU wave-instructions
 x active lanes, per segment, from the committed rocprofv3 PMC profile of the same build and
-workload) over the MI355X vector peak.  `cpu_baseline` times the CPU restatement of the
-reference (oracle/librtx_oracle.so) on a bounded band of the same frame on this host's
-available cores, with its calibration against the reference itself (profiles/
-cpu_calibration.json, scripts/calibrate_cpu.py), and `rms_vs_cpu` compares that band with
-the GPU's render of it by the same kernel build and schedule the timed frames used.
+workload) over the MI355X vector peak.  `cpu_baseline` times the reference itself
+(oracle/_ref/ref_harness: its own sources, its OpenMP loops) on the same frame at reduced spp
+on this host's available cores, with the CPU restatement (oracle/librtx_oracle.so, `port`)
+timed beside it on a bounded band, and `rms_vs_cpu` compares that band with the GPU's render
+of it by the same kernel build and schedule the timed frames used.
 """
 import argparse
 import json
@@ -43,7 +43,6 @@ WORKLOADS = {  # name -> (scene recipe, camera preset, width, spp, depth)
     "c4_bunny4k": ("bunny", "c4_bunny4k", 3840, 1024, 50),
     "c5_mixed": ("mixed", "c5_mixed", 3840, 2048, 50),
 }
-CALIBRATION_CASE = {"three": "c1_three", "final": "c2_final", "bunny": "c3_bunny", "mixed": "c5_mixed"}
 # MI355X_MICROARCH.md: 256 CUs x 4 SIMDs, 2400 MHz.  A SIMD retires 16 lanes of a VALU
 # operation per cycle, so a wave64 instruction holds it for 4 cycles (the issue-cost table:
 # v_add_f32 / v_fma_f32 4 cycles; PMC SQ_ACTIVE_INST_VALU counts one quad-cycle per
@@ -349,8 +348,17 @@ def main():
         if adaptive_leg:
             out["adaptive"] = adaptive_leg
         if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"], out["rms_vs_cpu"], out["rms_check"] = cpu_baseline(
+            port, out["rms_vs_cpu"], out["rms_check"] = cpu_baseline(
                 rtx, dev, host, cam, preset, scene_name, spp, depth, args, parked, build_bits)
+            # the reference itself (its own sources, oracle/_ref/ref_harness) timed here, on the
+            # same host cores: cpu_baseline; the port beside it (the RMS check's CPU side)
+            ref = cpu_reference(host, preset, W, spp, depth, args)
+            if ref is not None:
+                ref["port"] = port
+                ref["gpu_over_reference"] = out["value"] / ref["value"]
+                out["cpu_baseline"] = ref
+            else:
+                out["cpu_baseline"] = port
             rc = out["rms_check"]
             if args.adaptive and rc["rows"] == [0, H]:  # the CPU rendered the whole frame
                 rc["segments_gpu_recorded"] = int(cst["rays_recorded"])
@@ -471,6 +479,54 @@ def valu_roofline(workload, args, segs_per_launch, avg_launch_s):
                     "valu_issue_frac = issue cycles used incl. idle lanes / SIMD cycles"}
 
 
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+ASSETS = os.path.join(ROOT, "3360-ray-tracer_amd", "assets")
+
+
+def cpu_reference(host, preset, width, spp, depth, args):
+    """The reference's own renderer timed on this host: oracle/_ref/ref_harness (the reference's
+    CPURayIntegrator, BVH, materials and PixelState compiled from its sources by oracle/Makefile,
+    driven by the Render() glue of wavefront.cc:40-242) with its OpenMP IntersectBatch
+    (cpu_ray_integrator.h:24) and its parallel shading loop (wavefront.cc:105-217,
+    REF_PAR_SHADE=1) on the threads the port gets, at fixed spp on the whole frame.  A 1-spp
+    probe sizes the timed render to about 10 s.  None when the harness was not built (it needs
+    /root/reference at build time; the built binary travels with the tree)."""
+    import subprocess
+    import tempfile
+
+    if not os.path.exists(HARNESS):
+        return None
+    import oracle_ctypes as orc
+
+    threads = args.cpu_threads or available_cpus()
+    c = {"aspectRatio": 16 / 9.0, "vfov": 90.0, "defocusAngle": 0.0, "focusDist": 10.0}
+    c.update(orc.camera_preset(preset))
+    cam = [repr(float(c["aspectRatio"])), str(int(width)), repr(float(c["vfov"])),
+           *[repr(float(x)) for x in c["lookfrom"]], *[repr(float(x)) for x in c["lookat"]],
+           *[repr(float(x)) for x in c["vup"]], repr(float(c["defocusAngle"])), repr(float(c["focusDist"]))]
+    env = dict(os.environ, REF_THREADS=str(threads), REF_PAR_SHADE="1")
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "scene.rtxs")
+        host.write(path)
+
+        def run(n):
+            prefix = os.path.join(td, f"ref{n}")
+            subprocess.run([HARNESS, "render", path, ASSETS, *cam, str(depth), str(n), "0", str(args.seed), prefix],
+                           check=True, env=env, cwd=ASSETS, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                           timeout=300)
+            return dict(line.split() for line in open(prefix + ".stats"))
+
+        probe = run(1)
+        n = int(max(1, min(spp, 10.0 / max(float(probe["loop_seconds"]), 1e-3))))
+        st = run(n)
+    rays, sec = int(st["rays"]), float(st["loop_seconds"])
+    return {"value": rays / sec / 1e6, "unit": "Mrays/s", "cores": threads, "nproc": os.cpu_count(), "kind": "reference",
+            "sample": f"the whole {width}-wide frame at {n} spp (of {spp}), depth {depth}, fixed spp: {rays} segments "
+                      f"in {sec:.1f}s of the reference's pass loop (oracle/_ref/ref_harness: its own sources, OpenMP "
+                      f"IntersectBatch + parallel shading loop on {threads} threads, std::mt19937 per thread)",
+            "render_seconds_incl_p3": float(st["render_seconds"]), "threads_reported": int(st["threads"])}
+
+
 def cpu_baseline(rtx, dev, host, cam, preset, scene_name, spp, depth, args, parked, build_bits):
     """Time the CPU oracle on a centred band of the same frame; compare its pixels with the
     GPU's render of the band by the timed kernel build and schedule."""
@@ -509,36 +565,6 @@ def cpu_baseline(rtx, dev, host, cam, preset, scene_name, spp, depth, args, park
             "sample": f"{what} {W}x{H} frame, {spp} spp, depth {depth}, fixed spp, "
                       f"{st['rays']} segments in {dt:.1f}s (oracle/rtx_oracle.cc, OpenMP on {threads} threads, philox)"
                       .replace("fixed spp", sampling_text(args.adaptive))}
-    # the calibration measured with this many threads (scripts/calibrate_cpu.py --threads N on
-    # the GPU box's host, profiles/cpu_calibration_<N>t.json) when there is one
-    cal = os.path.join(ROOT, "profiles", f"cpu_calibration_{threads}t.json")
-    if not os.path.exists(cal):
-        cal = os.path.join(ROOT, "profiles", "cpu_calibration.json")
-    if os.path.exists(cal):
-        c = json.load(open(cal))
-        case = c["cases"].get(CALIBRATION_CASE.get(scene_name, ""))
-        if case:
-            r = case["ratio_port_over_reference"]
-            base["calibration"] = {
-                "ratio_port_over_reference": r, "case": case["config"], "threads": c["threads"],
-                "where": c["host"], "reference_mrays_s": case["reference"]["mrays_s"],
-                "port_mrays_s": case["port"]["mrays_s"],
-                "reference_parallel": c.get("reference_parallel", "IntersectBatch only"),
-                "reference_equivalent_value": base["value"] / r,
-                "note": "port and reference (its own sources, oracle/_ref) timed on identical configs and threads, the "
-                        "reference's shading loop parallel as wavefront.cc:105-217 runs it; reference_equivalent_value "
-                        "= value / ratio estimates the reference on these cores"}
-            # the same harness with the reference's shading loop run serially: on this host the
-            # reference is faster so (its OpenMP shading loop costs more than it gains), a
-            # conservative second estimate
-            ser = os.path.join(ROOT, "profiles", f"cpu_calibration_{threads}t_serial_shading.json")
-            if os.path.exists(ser):
-                sc = json.load(open(ser))["cases"].get(CALIBRATION_CASE.get(scene_name, ""))
-                if sc:
-                    base["calibration"]["serial_shading"] = {
-                        "ratio_port_over_reference": sc["ratio_port_over_reference"],
-                        "reference_mrays_s": sc["reference"]["mrays_s"],
-                        "reference_equivalent_value": base["value"] / sc["ratio_port_over_reference"]}
     check = {"mode": args.mode, "precision": args.precision, "schedule": sched,
              "kernel_build": rtx.build_names(gst["build"]), "same_build_as_timed": gst["build"] == build_bits,
              "rows": [tile[1], tile[1] + tile[3]],
