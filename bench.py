@@ -43,13 +43,19 @@ WORKLOADS = {  # name -> (scene recipe, camera preset, width, spp, depth)
     "c4_bunny4k": ("bunny", "c4_bunny4k", 3840, 1024, 50),
     "c5_mixed": ("mixed", "c5_mixed", 3840, 2048, 50),
 }
-# MI355X_MICROARCH.md: 256 CUs x 4 SIMDs, 2400 MHz.  A SIMD retires 16 lanes of a VALU
-# operation per cycle, so a wave64 instruction holds it for 4 cycles (the issue-cost table:
-# v_add_f32 / v_fma_f32 4 cycles; PMC SQ_ACTIVE_INST_VALU counts one quad-cycle per
-# instruction).  Vector peaks: FP64 78.6 TF = 1024 SIMDs x 16 lanes x 2 (FMA) x 2.4 GHz, FP32
-# 157.3 TF with packed FMA.  Non-packed f32 and f64 add / mul / fma issue at this rate.
-N_SIMD, CLOCK_HZ, LANES_PER_CYCLE, CYCLES_PER_VALU = 1024, 2.4e9, 16, 4
-VALU_PEAK_LANE_OPS = N_SIMD * LANES_PER_CYCLE * CLOCK_HZ  # 39.3e12 lane-ops/s
+# The VALU issue ceiling, MEASURED on gfx950 (scripts/microbench/valu_ceiling.hip, profiles/r05/
+# valu_ceiling_*.jsonl): with two or more waves per SIMD, a wave64 VALU instruction holds the
+# SIMD for one quad-cycle (4.1-4.3 cycles measured), except that two waves' all-VGPR
+# v_fma/add/mul_f32, v_add_u32, v_and_b32 and v_mov_b32 issue as a PAIR in one quad-cycle (2.3
+# cycles each: the guide's "2 cycles on SIMD-32", MI355X_MICROARCH.md:54); f64 add/mul/fma,
+# v_max/cmp/cndmask/cvt/bfe/med3/add_co/mul_u32_u24/mul_lo, packed f32 and 32-bit ops with an
+# SGPR operand never pair; transcendentals take 2 (f32) / 4 (f64) quad-cycles; one wave alone
+# gets ~4.6-5 cycles per instruction.  A mixed stream pairs almost nothing (3 f32 : 1 f64 FMAs:
+# 3.98 cycles per instruction).  PMC: SQ_ACTIVE_INST_VALU counts an instruction's quad-cycles,
+# SQ_ACTIVE_INST_VALU2 the quad-cycles in which a pair issued, so the SIMD's VALU issue
+# quad-cycles are their difference (checked against the measured cycles of every class within
+# ~5 %: the microbenchmark's per-class counters, pmc_r7a_valu_ceiling.csv).
+N_SIMD, CLOCK_HZ = 1024, 2.4e9
 HBM_PEAK_GBS = 8000.0
 STRIPE_ROWS = 8
 ADAPTIVE_MIN_SPP, ADAPTIVE_REL = 16, float(np.float32(0.05))  # wavefront.cc:42-43 (kRelThresh is a float)
@@ -450,33 +456,59 @@ def sampling_text(adaptive):
 
 
 def valu_roofline(workload, args, segs_per_launch, avg_launch_s):
-    """VALU-issue roofline of the hot kernel from the committed PMC profile of this build.
+    """VALU-issue roofline of the hot kernel from the committed PMC profile of this build and
+    workload (profiles/valu_<workload>_*.json, scripts/profile.sh) and the launch time measured
+    live (HIP events on the library's stream).
 
-    useful lane-ops / segment = SQ_INSTS_VALU x 64 x lane utilisation / segments, where lane
-    utilisation = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU) (PMC, same launch); achieved =
-    that x segments per launch (this run) / average launch time (this run, HIP events)."""
+    achieved = useful lane-ops per second: SQ_INSTS_VALU x 64 x lane utilisation per segment
+    (lane utilisation = SQ_THREAD_CYCLES_VALU / (64 x SQ_ACTIVE_INST_VALU)) x segments per launch
+    / launch time.  peak = the same instructions at the MEASURED best issue rate of their mix:
+    every instruction that may pair (all but the f64, 64-bit integer, conversion and
+    transcendental classes the PMC counts separately; an upper bound on what pairs, so the peak
+    is optimistic and frac conservative) at half a quad-cycle, the f64 / int64 / cvt ones at one,
+    transcendentals at 2 (f32) / 4 (f64), on 1024 SIMDs at 2.4 GHz.  frac = achieved / peak.
+    valu_issue_frac = the measured share of SIMD cycles issuing VALU work, 4 x (SQ_ACTIVE_INST_VALU
+    - SQ_ACTIVE_INST_VALU2) / SIMD cycles (idle lanes included)."""
     pf = os.path.join(ROOT, "profiles", f"valu_{workload}_{args.mode}_{args.precision}"
                       + ("_adaptive" if args.adaptive else "") + ".json")
-    base = {"bound": "valu", "peak": VALU_PEAK_LANE_OPS / 1e12, "unit": "Tlane-op/s (VALU)"}
+    base = {"bound": "valu", "unit": "Tlane-op/s (VALU)"}
     if not os.path.exists(pf):
-        return {**base, "achieved": None, "frac": None, "traffic": None, "note": f"no PMC profile {pf}"}
+        return {**base, "achieved": None, "peak": None, "frac": None, "traffic": None, "note": f"no PMC profile {pf}"}
     prof = json.load(open(pf))
     ops_per_seg = prof["lane_ops_per_segment"]
     insts_per_seg = prof["valu_insts_per_segment"]
     achieved = ops_per_seg * segs_per_launch / avg_launch_s
-    issue = insts_per_seg * segs_per_launch * CYCLES_PER_VALU / avg_launch_s / (N_SIMD * CLOCK_HZ)
     traffic = prof.get("hbm_bytes_per_segment")
-    return {**base, "achieved": achieved / 1e12, "frac": achieved / VALU_PEAK_LANE_OPS,
-            "traffic": traffic * segs_per_launch if traffic is not None else None,
-            "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, scaled to this launch)",
-            "hbm_GB_s": traffic * segs_per_launch / avg_launch_s / 1e9 if traffic is not None else None,
-            "hbm_frac": (traffic * segs_per_launch / avg_launch_s / 1e9 / HBM_PEAK_GBS) if traffic is not None else None,
-            "valu_issue_frac": issue, "lane_utilisation": prof["lane_utilisation"],
-            "lane_ops_per_segment": ops_per_seg, "valu_insts_per_segment": insts_per_seg,
-            "source": prof["source"],
-            "note": "VALU lane-ops: a wave64 VALU instruction holds a SIMD for 4 cycles (16 lanes/cycle); "
-                    "frac = useful (active-lane) operations / (1024 SIMDs x 16 lanes x 2.4 GHz); "
-                    "valu_issue_frac = issue cycles used incl. idle lanes / SIMD cycles"}
+    out = {**base, "achieved": achieved / 1e12, "peak": None, "frac": None,
+           "traffic": traffic * segs_per_launch if traffic is not None else None,
+           "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, scaled to this launch)",
+           "hbm_GB_s": traffic * segs_per_launch / avg_launch_s / 1e9 if traffic is not None else None,
+           "hbm_frac": (traffic * segs_per_launch / avg_launch_s / 1e9 / HBM_PEAK_GBS) if traffic is not None else None,
+           "lane_utilisation": prof["lane_utilisation"], "lane_ops_per_segment": ops_per_seg,
+           "valu_insts_per_segment": insts_per_seg, "source": prof["source"]}
+    n = prof.get("valu_insts_per_launch")
+    per = lambda k: prof.get(k + "_per_launch")  # noqa: E731
+    need = ["sq_active_inst_valu2", "sq_insts_valu_int64", "sq_insts_valu_cvt", "sq_insts_valu_trans_f32"]
+    if not n or any(per(k) is None for k in need):
+        out["note"] = "profile predates the dual-issue counters (SQ_ACTIVE_INST_VALU2): re-profile for peak / frac"
+        return out
+    f64 = per("sq_insts_valu_add_f64") + per("sq_insts_valu_mul_f64") + per("sq_insts_valu_fma_f64")
+    single = f64 + per("sq_insts_valu_int64") + per("sq_insts_valu_cvt")
+    trans32, trans64 = per("sq_insts_valu_trans_f32"), per("sq_insts_valu_trans_f64")
+    pairable = max(0.0, n - single - trans32 - trans64)
+    qmin = 0.5 * pairable + single + 2.0 * trans32 + 4.0 * trans64  # quad-cycles per launch at the best rate
+    peak = 64.0 * n / (4.0 * qmin / (N_SIMD * CLOCK_HZ))
+    quads = prof["active_inst_valu_per_launch"] - per("sq_active_inst_valu2")
+    segs_prof = prof["segments_per_launch"]
+    issue = 4.0 * quads / segs_prof * segs_per_launch / avg_launch_s / (N_SIMD * CLOCK_HZ)
+    out.update({"peak": peak / 1e12, "frac": achieved / peak, "valu_issue_frac": issue,
+                "pairable_share_max": pairable / n, "paired_share": 2.0 * per("sq_active_inst_valu2") / n,
+                "min_issue_ms": 4.0 * qmin / segs_prof * segs_per_launch / (N_SIMD * CLOCK_HZ) * 1e3,
+                "note": "peak: the profile's instruction mix at the measured gfx950 issue costs (pairs of 32-bit "
+                        "VOP2/VOP3 ops per quad-cycle, f64 / int64 / cvt one quad-cycle, transcendentals 2 / 4; "
+                        "scripts/microbench/valu_ceiling.hip) on 1024 SIMDs x 2.4 GHz; valu_issue_frac: "
+                        "4 x (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) / SIMD cycles"})
+    return out
 
 
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")

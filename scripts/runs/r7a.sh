@@ -12,3 +12,5 @@ export TMPDIR=/tmp
 echo "microbench done"
 timeout -k 10 900 bash scripts/profile.sh r7a_c3 --schedule park || exit 1
 echo "c3 profiled"
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -5 $O/pytest_gpu.log; exit 1; }
+tail -2 $O/pytest_gpu.log

@@ -29,7 +29,7 @@ def test_every_declared_symbol_is_exported(rtx_mod):
 
 
 def test_abi_version(rtx_mod):
-    assert rtx_mod.lib().rtx_abi_version() == 8
+    assert rtx_mod.lib().rtx_abi_version() == 9
 
 
 def test_library_is_a_gfx950_code_object(rtx_mod):
