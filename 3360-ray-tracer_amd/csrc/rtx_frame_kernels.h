@@ -261,7 +261,7 @@ struct AdaptPlan {
   int32_t predict_all;              // 1: a blocked pixel's next batch is predicted from all its ended samples
 };
 __device__ __forceinline__ uint32_t adapt_next_batch(const double (&mean)[3], const double (&m2)[3], int n,
-                                                     const AdaptPlan& ap) {
+                                                     const AdaptPlan& ap, bool raw = false) {
   double need = 0.0;  // samples at which IsConverged would hold with the current estimates
   for (int c = 0; c < 3; c++) {
     const double var = n > 1 ? m2[c] / (n - 1) : 0.0;
@@ -272,6 +272,7 @@ __device__ __forceinline__ uint32_t adapt_next_batch(const double (&mean)[3], co
   const double margin = 1.0 + ap.margin_step * (double)(ap.phase - 1);
   const double want = (need - (double)n) * margin;
   int k = (want < (double)left) ? (int)ceil(want) : left;  // NaN / inf: the whole budget
+  if (raw) return (uint32_t)max(0, min(k, min(left, ap.kcap)));
   k = max(k, min(max(4 << min(ap.phase - 1, 4), ap.kmin), left));  // at least 4, 8, ... 64 more, and kmin
   k = (k + 3) & ~3;
   return (uint32_t)min(k, min(left, ap.kcap));
@@ -335,7 +336,9 @@ __global__ __launch_bounds__(kBlock) void k_adapt_record(PixelSoA px, const doub
         }
       }
       const uint32_t alloc = (uint32_t)(s.n - r.n) <= pn ? pn - (uint32_t)(s.n - r.n) : 0u;  // allocated, not in s
-      const uint32_t want = adapt_next_batch(s.mean, s.m2, s.n, ap);  // (within budget - s.n)
+      // a blocked pixel gets more samples only where its prediction asks for more than it has
+      // allocated (no smallest batch: its pending samples are recorded next time anyway)
+      const uint32_t want = adapt_next_batch(s.mean, s.m2, s.n, ap, pn > 0 && ap.predict_all);
       kn = want > alloc ? min(want - alloc, (uint32_t)(ap.budget - r.n) - pn) : 0u;
       if (pn > 0 && ap.hold_blocked) kn = 0u;  // (a blocked pixel waits for its pending samples)
     }

@@ -90,6 +90,32 @@ def test_timed_kernel_builds_match_oracle(rtx_mod, orc, scenes, case, schedule):
     assert np.all(sp == spp) and st["rays_total"] == ref_st["rays"]
 
 
+# Whole frames at the configurations' own cameras and sizes against the oracle: C2 and C3 at
+# their full budgets (the benchmark's frames themselves), C4 and C5 at reduced spp (the oracle
+# finishes each in seconds on the box's host cores).  The benchmark's own schedule (auto).
+WHOLE_FRAME_CASES = [  # bench case index, spp
+    (0, 100),
+    (1, 200),
+    (2, 4),
+    (3, 2),
+]
+
+
+@pytest.mark.parametrize("wcase", WHOLE_FRAME_CASES, ids=[f"{BENCH_CASES[c[0]][1]}_{c[1]}spp" for c in WHOLE_FRAME_CASES])
+def test_whole_frame_matches_oracle(rtx_mod, orc, scenes, wcase):
+    ci, spp = wcase
+    scene, preset, width, _, depth, _, _ = BENCH_CASES[ci]
+    path, d = scenes(scene)
+    cam = rtx_mod.camera(rtx_mod.camera_config(preset, width=width))
+    ref, ref_spp, ref_st = oracle(orc, path, preset, width, spp, depth, 1234, None)
+    rgb, sp, st = d.render(cam, spp, depth, seed=1234, adaptive=False, mode="persistent", precision="fast",
+                           schedule="auto")
+    assert st["rays_total"] == ref_st["rays"], (st["rays_total"], ref_st["rays"])
+    assert np.all(sp == spp) and np.array_equal(sp, ref_spp.ravel())
+    rms = np.sqrt(np.mean((rgb - ref.reshape(-1, 3)) ** 2))
+    assert rms <= RMS_TOL, rms
+
+
 # The reference's default sampling (WavefrontRenderer::Render is always adaptive:
 # wavefront.cc:42-43 kRelThresh 0.05f / kMinSamples 16, converged pixels skipped at :68-69,
 # IsConverged at :125-127), on the timed builds at the configurations' own cameras and
