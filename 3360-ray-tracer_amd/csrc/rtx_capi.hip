@@ -114,6 +114,7 @@ float round_up(double x) {
 
 // statistics, queue counts, then the slot counter block (8 region counters 128 B apart, [128 + 4]
 // the segment buffer (0), ...)
+constexpr int kSlotBlockWords = 8 * 16 + 8;
 constexpr int kCounterWords = 64 + kSlotBlockWords;
 
 // Where a render's output goes once a band of it is final (fixed-spp renders): the
@@ -139,18 +140,8 @@ struct AdaptTune {
   int phase_kcap;       // phases: the largest batch of one pixel (else from the workspace)
   int first_map;         // the uniform first pass: 1 the phase kernel (block-shared chunks), 0 the uniform-group one (< 0: default)
   double phase_mstep;    // phases: the batch margin's growth per phase (< 0: kAdaptMarginStep)
-  int carry;             // 1: paths carried across phase launches, 0: every launch drains (< 0: kAdaptCarry)
-  int64_t final_slots;   // carried paths: the last phase once (pixels left) x (budget - min_spp) <= this (kAdaptFinalSlots)
-  int carry_until;       // carried paths out of launches 1 .. carry_until only (0: kAdaptCarryUntil)
-  int hold_blocked;      // a pixel with pending samples gets no further batch before they are recorded (< 0: kAdaptHold)
-  int predict_all;       // a blocked pixel's next batch from all its ended samples (< 0: kAdaptPredictAll)
 };
-static AdaptTune g_tune{0, 0, -1, -1.0, -1, 0, 0, -1, -1};
-constexpr bool kAdaptPredictAll = true;
-constexpr int kAdaptCarryUntil = 1 << 30;
-constexpr bool kAdaptHold = false;
-constexpr int64_t kAdaptFinalSlots = 3ll << 22;  // render_adaptive: see k_adapt_floor
-constexpr bool kAdaptCarry = true;  // render_adaptive: phase launches carry their unfinished paths over
+static AdaptTune g_tune{0, 0, -1, -1.0};
 constexpr int kFirstPassMap = 1;  // the adaptive first pass runs the phase kernel (MAP 1, no slot map)
 // RTX_DEBUG_HOST: host-side timestamps of a frame (render_stripes_to_host prints them, with the
 // device; per thread: rtx_render_multi renders each device on a thread of its own)
@@ -160,18 +151,12 @@ static double host_us() {
 }
 static thread_local double g_t_launch = 0, g_t_sync0 = 0, g_t_sync1 = 0;
 struct AdaptWs {
-  // lbuf: the phases' radiance records, two halves (phase g uses half g & 1: a phase's records
-  // stay while the next phase runs, for the samples the record left pending); smap: the next
-  // phase's slot map; k[2], off: batch sizes and offsets; pend[4]: the pending samples (slot,
-  // count) out of record g in pend[2 (g & 1)], pend[2 (g & 1) + 1]; carry[2]: the carry queues;
-  // ctr: the slot counter block (rtx_kernels.h kSlotW*)
-  DevBuf lbuf, smap, k[2], off, scan_tmp, ctr, pend[4], carry[2];
-  DevBuf segs;                                  // counting renders: each slot's path segments (u16), two halves
-  HostBuf total_h;                              // pinned copy of the counter block's words 128 .. 142 after each record
+  DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer
+  DevBuf segs;                                  // counting renders: each slot's path segments (u16)
+  HostBuf total_h;                              // pinned copy of the next phase's slot count
   hipEvent_t ev = nullptr;                      // total_h written
   void release() {
-    for (DevBuf* b : {&lbuf, &smap, &k[0], &k[1], &off, &scan_tmp, &ctr, &segs, &pend[0], &pend[1], &pend[2],
-                      &pend[3], &carry[0], &carry[1]})
+    for (DevBuf* b : {&lbuf, &smap, &k[0], &k[1], &off, &scan_tmp, &ctr, &segs})
       b->release();
     total_h.release();
     if (ev) (void)hipEventDestroy(ev);
@@ -184,6 +169,7 @@ struct rtx_scene {
   hipStream_t stream = nullptr;
   int cus = 0;
   DevBuf nodes, prims, mats, texs, images, fnodes, tri_n;
+  DevBuf segs1;  // counting adaptive renders: the first phase's per-slot path segments (u16)
   std::vector<DevBuf> texels;
   DScene S{};
   int stack_parity = 32, stack_fast = 32;
@@ -545,9 +531,8 @@ double slot_allowance(rtx_scene* sc) {
       (void)hipGetLastError();
       fr = (size_t)1 << 62;
     }
-    double held = (double)sc->lbuf.n + (double)sc->queue[0].n + (double)sc->queue[1].n;
-    held += (double)sc->aw.lbuf.n + (double)sc->aw.smap.n + (double)sc->aw.segs.n + (double)sc->aw.carry[0].n +
-            (double)sc->aw.carry[1].n;
+    double held = (double)sc->lbuf.n + (double)sc->queue[0].n + (double)sc->queue[1].n + (double)sc->segs1.n;
+    held += (double)sc->aw.lbuf.n + (double)sc->aw.smap.n + (double)sc->aw.segs.n;
     sc->slot_mem = 0.5 * ((double)fr + held);
   }
   return sc->slot_mem;
@@ -733,10 +718,10 @@ int persist_m(const Launch& L, const RenderArgs& A, unsigned long long* ns) {
 int time_park_schedule(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm, hipStream_t s);
 
 // Counting renders: the persistent launch's slot counter block names the buffer its paths'
-// segment counts go to (k_persistent COUNT builds read word kSlotWSegs of it).
+// segment counts go to (k_persistent COUNT builds read word 8 * 16 + 4 of it).
 int set_segbuf(unsigned long long* ctr, uint16_t* segs, hipStream_t st) {
   const unsigned long long v = (unsigned long long)(uintptr_t)segs;
-  uint32_t* w = (uint32_t*)(ctr + kSlotWSegs);  // (two 32-bit memsets: stream-ordered, no host staging)
+  uint32_t* w = (uint32_t*)(ctr + 8 * 16 + 4);  // (two 32-bit memsets: stream-ordered, no host staging)
   HIPC(hipMemsetD32Async((hipDeviceptr_t)w, (int)(uint32_t)v, 1, st));
   HIPC(hipMemsetD32Async((hipDeviceptr_t)(w + 1), (int)(uint32_t)(v >> 32), 1, st));
   return RTX_OK;
@@ -746,11 +731,8 @@ int set_segbuf(unsigned long long* ctr, uint16_t* segs, hipStream_t st) {
 // stream `s`.  Phase 1 traces min_spp samples of every pixel (one uniform launch) and
 // k_adapt_record replays them and sizes each pixel's next batch.  After each phase, record +
 // next batch sizes (k_adapt_record, k_adapt_floor); before each phase, prefix sum and slot map
-// (k_adapt_expand); the host reads the next phase's slot count (pinned words) to launch it or
-// stop.  With carried paths (kAdaptCarry, rtx_kernels.h) a phase launch ends once its slots
-// are used up, its unfinished paths carried over to the next launch, which resumes them first;
-// the record leaves the samples they belong to pending until they have ended.  The last launch
-// (no fresh slots left) drains.  Without them every phase launch drains on its own.
+// (k_adapt_expand); the host reads the next phase's slot count (one pinned word) to launch it
+// or stop; every phase is a launch of its own with its own drain.
 // `mark` records a hot-kernel timing event (before and after each persistent launch);
 // hot_launches counts them.  The caller resolves the pixels (k_resolve).
 template <class Mark>
@@ -760,44 +742,34 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   const int K1 = std::min(std::max(1, prm->min_spp), budget);
   static const bool debug = std::getenv("RTX_DEBUG_ADAPT") != nullptr;  // per-phase slot counts on stderr
   const int64_t phase_slots = g_tune.phase_slots > 0 ? g_tune.phase_slots : kAdaptPhaseSlots;
-  const bool carry = g_tune.carry >= 0 ? g_tune.carry != 0 : kAdaptCarry;
-  // carried paths: the phase after which at most this many pixels are left is the last
-  const int64_t final_px =
-      (g_tune.final_slots > 0 ? g_tune.final_slots : kAdaptFinalSlots) / std::max(1, budget - std::max(0, prm->min_spp));
+  if ((int64_t)npix * K1 > 0xFFFFFFFFll) return fail(RTX_ERR_INVALID, "adaptive render: npix x min_spp above 2^32");
   AdaptWs& w = sc->aw;
   int rc;
-  // per slot of a half: 2 x 24 B of radiance (two halves) + 8 B of slot map (+ 2 x 2 B of segments)
-  // (within the allowance less the buffers of other kinds the scene keeps: render_device_impl)
-  const int64_t cap = std::min<int64_t>(
-      1ll << 30, slot_target(sc, 56 + (L.count ? 4 : 0), 1ll << kSlotTargetLog2,
-                             (double)npix * 5 * 2 * sizeof(uint32_t) + (double)sc->lbuf.n + (double)sc->queue[0].n +
-                                 (double)sc->queue[1].n));
-  if (npix * std::max(4, K1) > cap) return fail(RTX_ERR_NOMEM, "adaptive render: too many pixels for the device memory");
+  // the uniform first pass's radiance (and segment) records, in the scene's buffers
+  const double first_bytes = (double)npix * K1 * (3 * sizeof(double) + (L.count ? 2 : 0));
+  // slots after the first phase: 24 B of radiance + 8 B of slot map each (+ 2 B of segments)
+  const int64_t cap =
+      std::min<int64_t>(0xFFFFFFFFll, slot_target(sc, 32 + (L.count ? 2 : 0), 1ll << kSlotTargetLog2, first_bytes));
+  if (npix * 4 > cap) return fail(RTX_ERR_NOMEM, "adaptive render: too many pixels for the device memory");
   int32_t kcap = (int32_t)std::min<int64_t>(budget, std::max<int64_t>(4, (cap / npix) & ~3ll));
   if (g_tune.phase_kcap > 0) kcap = std::min(kcap, g_tune.phase_kcap);
-  const int64_t H = npix * (int64_t)std::max(kcap, K1);  // slots per half (phase 1 takes npix x K1 of its half)
-  const uint32_t qcap = 2048u * (uint32_t)std::max(1, sc->cus);  // carry queue entries: every lane of the grid
   {
-    if ((rc = w.lbuf.reserve(2 * H * 3 * sizeof(double)))) return rc;
-    if (L.count && (rc = w.segs.reserve(2 * H * sizeof(uint16_t)))) return rc;
-    if ((rc = w.smap.reserve(H * sizeof(uint2)))) return rc;
-    for (DevBuf* b : {&w.k[0], &w.k[1], &w.off, &w.pend[0], &w.pend[1], &w.pend[2], &w.pend[3]})
+    const int64_t slots = npix * (int64_t)kcap;
+    if ((rc = w.lbuf.reserve(slots * 3 * sizeof(double)))) return rc;
+    if (L.count && (rc = w.segs.reserve(slots * sizeof(uint16_t)))) return rc;
+    if ((rc = w.smap.reserve(slots * sizeof(uint2)))) return rc;
+    for (DevBuf* b : {&w.k[0], &w.k[1], &w.off})
       if ((rc = b->reserve(npix * sizeof(uint32_t)))) return rc;
-    for (DevBuf* b : {&w.carry[0], &w.carry[1]})
-      if ((rc = b->reserve(carry_queue_bytes(qcap)))) return rc;
     if ((rc = w.scan_tmp.reserve(std::max<size_t>(16, rtxscan::temp_bytes(npix))))) return rc;
-    if ((rc = w.ctr.reserve(kSlotBlockWords * sizeof(unsigned long long)))) return rc;
-    if ((rc = w.total_h.reserve(16 * sizeof(unsigned long long)))) return rc;
+    if ((rc = w.ctr.reserve(8 * 16 * sizeof(unsigned long long) + 64))) return rc;
+    if ((rc = w.total_h.reserve(2 * sizeof(unsigned long long)))) return rc;
     if (!w.ev) HIPC(hipEventCreateWithFlags(&w.ev, hipEventDisableTiming));
   }
-  unsigned long long* ctr = w.ctr.as<unsigned long long>();  // the slot counter block (kSlotW*)
-  HIPC(hipMemsetAsync(ctr, 0, kSlotBlockWords * sizeof(unsigned long long), s));
+  unsigned long long* ctr = w.ctr.as<unsigned long long>();  // 8 region counters, then the slot count, ...
   const unsigned qb = (unsigned)((npix + kBlock - 1) / kBlock);
-  auto half = [&](int g) { return (uint32_t)((g & 1) * H); };  // phase g's first radiance slot
-  // record + next batch sizes after phase g (its slots in its half: the uniform first phase's
-  // p * K1 + k, or the phase's slot map), then the next phase's prefix sum, slot map and (to the
-  // host) slot count, pixel count and carried paths
-  auto record = [&](int g, int64_t active) -> int {
+  // record + next batch sizes after phase g (its slots in Lph: the uniform first phase's, or the
+  // phase's slot map), then the next phase's prefix sum, slot map and (to the host) slot count
+  auto record = [&](int g, const double* Lph, int64_t active) -> int {
     AdaptPlan ap;
     ap.kcur = g == 1 ? nullptr : w.k[g & 1].as<uint32_t>();
     ap.off = g == 1 ? nullptr : w.off.as<uint32_t>();
@@ -809,44 +781,33 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ap.kmin = (int32_t)std::min<int64_t>(budget, (phase_slots + active - 1) / std::max<int64_t>(1, active));
     ap.rel = prm->rel_threshold;
     ap.margin_step = g_tune.phase_mstep >= 0 ? g_tune.phase_mstep : kAdaptMarginStep;
-    ap.segs = L.count ? w.segs.as<uint16_t>() : nullptr;
+    ap.segs = !L.count ? nullptr : g == 1 ? sc->segs1.as<uint16_t>() : w.segs.as<uint16_t>();
     ap.rec_segs = A.counters + 9;
-    ap.active = ctr + kSlotWCount + 1;
-    ap.next_active = ctr + kSlotWCount + 3;
+    ap.active = ctr + 8 * 16 + 1;
+    ap.next_active = ctr + 8 * 16 + 3;
     // (ap.next_active was zeroed with the phase's slot counter block, k_slot_block_init)
-    ap.lbase = half(g);
-    ap.pin_off = carry && g > 1 ? w.pend[2 * ((g - 1) & 1)].as<uint32_t>() : nullptr;
-    ap.pin_k = carry && g > 1 ? w.pend[2 * ((g - 1) & 1) + 1].as<uint32_t>() : nullptr;
-    ap.pout_off = carry ? w.pend[2 * (g & 1)].as<uint32_t>() : nullptr;
-    ap.pout_k = carry ? w.pend[2 * (g & 1) + 1].as<uint32_t>() : nullptr;
-    ap.err = ctr + kSlotWCount + 6;
-    ap.hold_blocked = (g_tune.hold_blocked >= 0 ? g_tune.hold_blocked != 0 : kAdaptHold) ? 1 : 0;
-    ap.predict_all = (g_tune.predict_all >= 0 ? g_tune.predict_all != 0 : kAdaptPredictAll) ? 1 : 0;
-    hipLaunchKernelGGL(k_adapt_record, dim3(qb), dim3(kBlock), 0, s, px, (const double*)w.lbuf.as<double>(), npix,
-                       npix, ap);
+    hipLaunchKernelGGL(k_adapt_record, dim3(qb), dim3(kBlock), 0, s, px, Lph, npix, npix, ap);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_adapt_floor, dim3(qb), dim3(kBlock), 0, s, ap.knext, npix, 1, 0, (const int32_t*)px.samples,
-                       (const uint32_t*)ap.pout_k, budget, kcap, phase_slots, carry ? final_px : (int64_t)-1, ctr);
+                       budget, kcap, phase_slots, (const unsigned long long*)ap.next_active);
     HIPC(hipGetLastError());
     HIPC(rtxscan::exclusive_scan_u32(ap.knext, w.off.as<uint32_t>(), npix, w.scan_tmp.p, w.scan_tmp.n, s));
     hipLaunchKernelGGL(k_adapt_expand, dim3((unsigned)((npix + kExpandPix - 1) / kExpandPix)), dim3(kBlock), 0, s,
-                       (const uint32_t*)ap.knext, (const uint32_t*)w.off.as<uint32_t>(), npix, 1, 0,
-                       (const int32_t*)px.samples, (const uint32_t*)ap.pout_k, w.smap.as<uint2>(), ctr + kSlotWCount);
+                       (const uint32_t*)ap.knext,
+                       (const uint32_t*)w.off.as<uint32_t>(), npix, 1, 0, (const int32_t*)px.samples,
+                       w.smap.as<uint2>(), ctr + 8 * 16);
     HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(w.total_h.p, ctr + kSlotWCount, 15 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPC(hipMemcpyAsync(w.total_h.p, ctr + 8 * 16, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     HIPC(hipEventRecord(w.ev, s));
     return RTX_OK;
   };
   // one persistent launch of a phase; debug: its time and segments on stderr
   // uniform: the launch's slot count (no slot map: uniform groups); 0: the slot map's, from k_adapt_expand
-  auto launch = [&](int g, const Launch& Lg, const RenderArgs& Ag, int64_t pixels, bool carry_out,
-                    uint64_t uniform = 0, size_t seg_off = 0) -> int {
+  auto launch = [&](int g, const Launch& Lg, const RenderArgs& Ag, uint16_t* segs, int64_t pixels,
+                    uint64_t uniform = 0) -> int {
     unsigned long long seg0 = 0;
-    SlotBlockInit bi{};
-    bi.nslots = uniform, bi.smap = 0, bi.lbase = half(g);
-    bi.cin = (unsigned long long)w.carry[(g + 1) & 1].p, bi.cout = (unsigned long long)w.carry[g & 1].p;
-    bi.cap = qcap, bi.flags = carry_out ? 1ull : 0ull, bi.set = uniform ? 1 : 0, bi.first = g == 1;
-    hipLaunchKernelGGL(k_slot_block_init, dim3(1), dim3(8 * 16), 0, s, ctr, bi);
+    hipLaunchKernelGGL(k_slot_block_init, dim3(1), dim3(8 * 16), 0, s, ctr, uniform ? 1 : 0,
+                       (unsigned long long)uniform, 0ull);
     HIPC(hipGetLastError());
     if (debug) {
       HIPC(hipStreamSynchronize(s));
@@ -856,7 +817,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     int rc2;
     if (debug) HIPC(hipMemsetAsync(A.counters + 13, 0, 5 * sizeof(unsigned long long), s));  // (the timeline)
     if ((rc2 = mark(s))) return rc2;
-    if (L.count && (rc2 = set_segbuf(ctr, w.segs.as<uint16_t>() + seg_off, s))) return rc2;
+    if (L.count && (rc2 = set_segbuf(ctr, segs, s))) return rc2;
     if ((rc2 = persist_m<false>(Lg, Ag, ctr))) return rc2;
     L.build = Lg.build;  // (the stats report the instantiation launched last)
     if ((rc2 = mark(s))) return rc2;
@@ -865,10 +826,9 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
       HIPC(hipEventRecord(sc->ev[3], s));
       HIPC(hipEventSynchronize(sc->ev[3]));
       float ms = 0;
-      unsigned long long seg1 = 0, blk[16] = {};
+      unsigned long long seg1 = 0;
       HIPC(hipEventElapsedTime(&ms, sc->ev[2], sc->ev[3]));
       HIPC(hipMemcpy(&seg1, A.counters, sizeof seg1, hipMemcpyDeviceToHost));
-      HIPC(hipMemcpy(blk, ctr + kSlotWCount, sizeof blk, hipMemcpyDeviceToHost));
       unsigned long long tt[18] = {};
       HIPC(hipMemcpy(tt, A.counters, sizeof tt, hipMemcpyDeviceToHost));
       if (tt[13]) {  // counting build: the launch's timeline (us from the first block's start)
@@ -877,44 +837,41 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
         fprintf(stderr, "rtx adaptive: phase %d timeline: slots used up %.1f .. %.1f us, waves end %.1f .. %.1f us\n",
                 g, us(~tt[15]), us(tt[14]), us(~tt[17]), us(tt[16]));
       }
-      fprintf(stderr,
-              "rtx adaptive: phase %d: %lld pixels, %llu slots, %llu paths carried in, %llu carried out, launch %.3f ms, "
-              "%llu segments (%.0f Mseg/s)\n",
-              g, (long long)pixels, blk[0], blk[kSlotWCinCount - kSlotWCount], blk[kSlotWCoutCount - kSlotWCount], ms,
-              seg1 - seg0, (double)(seg1 - seg0) / (ms * 1e3));
+      fprintf(stderr, "rtx adaptive: phase %d: %lld pixels, launch %.3f ms, %llu segments (%.0f Mseg/s)\n", g,
+              (long long)pixels, ms, seg1 - seg0, (double)(seg1 - seg0) / (ms * 1e3));
     }
     return RTX_OK;
   };
-  // phase 1: min_spp samples of every pixel, one uniform launch over the whole render
-  RenderArgs Ag = A;
-  Ag.L = w.lbuf.as<double>();  // (every phase: radiance slots of the two halves)
-  Ag.conv = nullptr;           // only pixels still sampling have slots
-  Ag.K = K1, Ag.s0 = 0;        // (the first phase's uniform groups; later phases read the slot map)
+  // phase 1: min_spp samples of every pixel, one uniform launch over the whole render (the
+  // scene's radiance buffer)
+  if ((rc = sc->lbuf.reserve((size_t)npix * K1 * 3 * sizeof(double)))) return rc;
+  if (L.count && (rc = sc->segs1.reserve((size_t)npix * K1 * sizeof(uint16_t)))) return rc;
+  RenderArgs A1 = A;
+  A1.L = sc->lbuf.as<double>();
+  A1.conv = nullptr;
+  A1.K = K1, A1.s0 = 0;
   // the phase kernel without a slot map (uniform groups: slot p * K1 + k), for its block-shared
-  // chunks and carried paths
+  // chunks: the first pass ends as the phases do, its last slots traced by whole blocks
   Launch L1 = L;
-  const bool first_map1 = carry || (g_tune.first_map >= 0 ? g_tune.first_map : kFirstPassMap) == 1;
+  const bool first_map1 = (g_tune.first_map >= 0 ? g_tune.first_map : kFirstPassMap) == 1;
   if (first_map1) L1.map = 1;
-  else Ag.L = w.lbuf.as<double>() + 3 * (size_t)half(1);  // (the uniform-group kernel: no radiance base word)
-  if ((rc = launch(1, L1, Ag, npix, carry, first_map1 ? (uint64_t)npix * (uint64_t)K1 : 0, first_map1 ? 0 : half(1))))
+  if ((rc = launch(1, L1, A1, sc->segs1.as<uint16_t>(), npix, first_map1 ? (uint64_t)npix * (uint64_t)K1 : 0)))
     return rc;
+  if ((rc = record(1, sc->lbuf.as<double>(), npix))) return rc;
+  RenderArgs Ag = A;
   Ag.L = w.lbuf.as<double>();
-  if ((rc = record(1, npix))) return rc;
+  Ag.conv = nullptr;    // only pixels still sampling have slots
   Ag.K = 1, Ag.s0 = 0;  // (unused: slots from the phase's slot map)
   Launch Lg = L;
   Lg.map = 1;
   for (int g = 2;; g++) {
-    // this phase's slot count and pixels, and the paths the last launch carried over
+    // this phase's slot count, computed at the end of the previous one
     HIPC(hipEventSynchronize(w.ev));
-    const volatile unsigned long long* th = (const volatile unsigned long long*)w.total_h.p;
-    const unsigned long long nsl = th[0], carried = th[kSlotWCoutCount - kSlotWCount];
-    const int64_t active = (int64_t)th[1];
-    if (th[6]) return fail(RTX_ERR_HIP, "adaptive render: a pending sample's path had not ended");
-    if (nsl == 0 && carried == 0) break;
-    // a launch with fresh slots carries its unfinished paths over; one with only carried paths drains
-    const int until = g_tune.carry_until > 0 ? g_tune.carry_until : kAdaptCarryUntil;
-    if ((rc = launch(g, Lg, Ag, active, carry && nsl > 0 && g <= until))) return rc;
-    if ((rc = record(g, std::max<int64_t>(1, active)))) return rc;
+    const unsigned long long nsl = ((const volatile unsigned long long*)w.total_h.p)[0];
+    const int64_t active = (int64_t)((const volatile unsigned long long*)w.total_h.p)[1];
+    if (nsl == 0) break;
+    if ((rc = launch(g, Lg, Ag, w.segs.as<uint16_t>(), active))) return rc;
+    if ((rc = record(g, Ag.L, active))) return rc;
   }
   return RTX_OK;
 }
@@ -1276,25 +1233,22 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   const bool phased = prm->mode == RTX_MODE_PERSISTENT && prm->adaptive && !mk_adaptive &&
                       prm->samples_per_group <= 0 && budget > 0 && npix > 0;
   // One allowance (slot_allowance) for all of a scene's slot buffers: the radiance buffer of
-  // uniform groups (lbuf), the wavefront's path queues, the adaptive phases' workspace (aw).  A
-  // render keeps the other kinds' buffers as long as they and what it needs itself fit in the
-  // allowance, and releases them only when they do not: every release and reallocation
-  // synchronises the device, and frames that alternate kinds (the bench's fixed-spp line, its
-  // adaptive leg, the CPU check) would pay it every time.  (The adaptive workspace sizes itself
-  // in what is left; its need here is its largest size.)
-  const double queue_bytes = (double)sc->queue[0].n + (double)sc->queue[1].n;
-  const double aw_bytes = (double)sc->aw.lbuf.n + (double)sc->aw.smap.n + (double)sc->aw.segs.n +
-                          (double)sc->aw.carry[0].n + (double)sc->aw.carry[1].n;
+  // uniform groups and of the adaptive first pass (lbuf), the wavefront's path queues, the
+  // adaptive phases' workspace (aw).  A render keeps the other kinds' buffers as long as they
+  // and what it needs itself fit in the allowance, and releases them only when they do not:
+  // every release and reallocation synchronises the device, and frames that alternate kinds
+  // (the bench's fixed-spp line, its adaptive leg, the CPU check) would pay it every time.
   double other = 0.0;  // bytes of other kinds kept
   {
-    const double allow = slot_allowance(sc);
-    const double per_slot = phased ? 56.0 : prm->mode == RTX_MODE_WAVEFRONT ? 24.0 + 2 * 84.0 : 24.0;
-    const double want = per_slot * (double)npix * (double)std::max(1, budget);
     const bool wf = prm->mode == RTX_MODE_WAVEFRONT;
-    other = (phased ? (double)sc->lbuf.n : aw_bytes) + (wf ? 0.0 : queue_bytes);
+    const double allow = slot_allowance(sc);
+    const double per_slot = phased ? 34.0 : wf ? 24.0 + 2 * 84.0 : 24.0;  // (phases: radiance, slot map, batches)
+    const double want = per_slot * (double)npix * (double)std::max(1, budget);
+    const double aw_bytes = (double)sc->aw.lbuf.n + (double)sc->aw.smap.n + (double)sc->aw.segs.n;
+    const double queue_bytes = (double)sc->queue[0].n + (double)sc->queue[1].n;
+    other = (phased ? 0.0 : aw_bytes) + (wf ? 0.0 : queue_bytes);
     if (other + std::min(want, per_slot * (double)(1ll << kSlotTargetLog2)) > allow) {
-      if (phased) sc->lbuf.release();
-      else sc->aw.release();
+      if (!phased) sc->aw.lbuf.release(), sc->aw.smap.release(), sc->aw.segs.release();
       if (!wf)
         for (auto& q : sc->queue) q.release();
       other = 0.0;
@@ -1881,18 +1835,12 @@ extern "C" int rtx_internal_check_sincos(int device, int64_t n, uint64_t seed, i
 // Test / tuning hook (not in rtx.h): overrides of the adaptive phases' constants for the
 // renders that follow in this process (0 / negative restores a default): the smallest phase,
 // the largest batch of a pixel, the first pass's kernel (1 the phase kernel, 0 the uniform-group
-// one; with carried paths always the phase kernel), the batch margin's growth per phase,
-// carried paths (1 on, 0 every phase launch drains) and the last phase's size (final_slots).  Results never depend on them, only the
-// amount of work and the number of phases do (tests/test_gpu_timed.py runs the full budgets
-// through forced small workspaces).
-extern "C" int rtx_internal_adapt_tune(int64_t phase_slots, int32_t phase_kcap, int32_t first_map, double phase_mstep,
-                                       int32_t carry, int64_t final_slots, int32_t carry_until, int32_t hold_blocked,
-                                       int32_t predict_all) {
-  if (phase_slots < 0 || phase_kcap < 0 || first_map > 1 || carry > 1 || final_slots < 0 || carry_until < 0 ||
-      hold_blocked > 1 || predict_all > 1)
-    return fail(RTX_ERR_INVALID, "bad tuning value");
-  g_tune = AdaptTune{phase_slots, phase_kcap, first_map, phase_mstep, carry, final_slots, carry_until, hold_blocked,
-                     predict_all};
+// one) and the batch margin's growth per phase.  Results never depend on them, only the amount
+// of work and the number of phases do (tests/test_gpu_timed.py runs the full budgets through
+// forced small workspaces).
+extern "C" int rtx_internal_adapt_tune(int64_t phase_slots, int32_t phase_kcap, int32_t first_map, double phase_mstep) {
+  if (phase_slots < 0 || phase_kcap < 0 || first_map > 1) return fail(RTX_ERR_INVALID, "bad tuning value");
+  g_tune = AdaptTune{phase_slots, phase_kcap, first_map, phase_mstep};
   return RTX_OK;
 }
 

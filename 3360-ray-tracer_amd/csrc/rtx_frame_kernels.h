@@ -98,11 +98,9 @@ struct PixRec {
   int n;
   bool conv;
 };
-// Returns the samples replayed; stops early at convergence, or (blocked = true) at a radiance
-// record that still holds kCarrySentinel: a carried path that has not ended yet.
 template <int AHEAD>
-__device__ __forceinline__ int replay_pixel(PixRec& r, const double* __restrict__ Lp, int K, int min_spp,
-                                            double rel, bool& blocked) {
+__device__ __forceinline__ void replay_pixel(PixRec& r, const double* __restrict__ Lp, int K, int min_spp,
+                                             double rel) {
   auto record = [&](const double (&x)[3]) {
     r.n++;
     for (int c = 0; c < 3; c++) {
@@ -146,22 +144,14 @@ __device__ __forceinline__ int replay_pixel(PixRec& r, const double* __restrict_
   };
 #pragma unroll
   for (int i = 0; i < AHEAD; i++) load(i, i);
-  int done = 0;
-  blocked = false;
-  for (int k = 0; k < K && !r.conv && !blocked; k += AHEAD) {
+  for (int k = 0; k < K && !r.conv; k += AHEAD) {
 #pragma unroll
     for (int i = 0; i < AHEAD; i++) {
       if (k + i >= K || r.conv) break;
-      if ((uint64_t)__double_as_longlong(b[i][0]) == kCarrySentinel) {
-        blocked = true;
-        break;
-      }
       record(b[i]);
-      done++;
       load(i, k + i + AHEAD);
     }
   }
-  return done;
 }
 __device__ __forceinline__ void load_pixel(PixRec& r, const PixelSoA& px, int64_t npix, int64_t p) {
   for (int c = 0; c < 3; c++) r.sum[c] = px.sum[c * npix + p], r.mean[c] = px.mean[c * npix + p], r.m2[c] = px.m2[c * npix + p];
@@ -232,12 +222,6 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(PixelSoA px, const double
 // (pixel, sample).  Only pixels still sampling get slots.  A sample traced past its pixel's
 // convergence point is discarded here, so the result is the reference's whatever the batch
 // sizes are: the prediction only decides how much work is spent and how many phases it takes.
-//
-// With paths carried across launches (rtx_kernels.h), the record stops a pixel at its first
-// sample whose path has not ended (kCarrySentinel) and leaves that sample and the rest of its
-// batch pending; the next record replays the pending samples first (their paths have ended by
-// then: they were resumed by the next launch), then the next batch.  The pixel's next batch
-// is its predicted need less what is pending, its first sample after the pending ones.
 // ---------------------------------------------------------------------------------------
 struct AdaptPlan {
   const uint32_t* kcur;  // samples of sub-pixel q in the phase just traced (nullptr: kuni each)
@@ -253,15 +237,9 @@ struct AdaptPlan {
   unsigned long long* rec_segs;   // ... summed here over the samples the pixels record
   unsigned long long* active;  // the next phase's pixel count (k_adapt_expand adds; zeroed here)
   unsigned long long* next_active;  // ... counted here too (zeroed before the launch), for k_adapt_floor
-  uint32_t lbase;                   // the radiance slot of the phase's local slot 0 (kcur / off / kuni are local)
-  const uint32_t *pin_off, *pin_k;  // samples left pending by the previous record (radiance slot, count), or nullptr
-  uint32_t *pout_off, *pout_k;      // out: the samples this record leaves pending
-  unsigned long long* err;          // set when a pending sample's path had not ended (never: the schedule's invariant)
-  int32_t hold_blocked;             // 1: a pixel with pending samples gets no further batch until they are recorded
-  int32_t predict_all;              // 1: a blocked pixel's next batch is predicted from all its ended samples
 };
 __device__ __forceinline__ uint32_t adapt_next_batch(const double (&mean)[3], const double (&m2)[3], int n,
-                                                     const AdaptPlan& ap, bool raw = false) {
+                                                     const AdaptPlan& ap) {
   double need = 0.0;  // samples at which IsConverged would hold with the current estimates
   for (int c = 0; c < 3; c++) {
     const double var = n > 1 ? m2[c] / (n - 1) : 0.0;
@@ -272,7 +250,6 @@ __device__ __forceinline__ uint32_t adapt_next_batch(const double (&mean)[3], co
   const double margin = 1.0 + ap.margin_step * (double)(ap.phase - 1);
   const double want = (need - (double)n) * margin;
   int k = (want < (double)left) ? (int)ceil(want) : left;  // NaN / inf: the whole budget
-  if (raw) return (uint32_t)max(0, min(k, min(left, ap.kcap)));
   k = max(k, min(max(4 << min(ap.phase - 1, 4), ap.kmin), left));  // at least 4, 8, ... 64 more, and kmin
   k = (k + 3) & ~3;
   return (uint32_t)min(k, min(left, ap.kcap));
@@ -289,62 +266,23 @@ __global__ __launch_bounds__(kBlock) void k_adapt_record(PixelSoA px, const doub
   if (q >= nq) return;
   const int64_t p = q * ap.sub_n + ap.sub_j;
   const int K = ap.kcur ? (int)ap.kcur[q] : ap.kuni;
-  const int pk = ap.pin_k ? (int)ap.pin_k[q] : 0;
-  uint32_t kn = 0, po = 0, pn = 0;
-  if ((K > 0 || pk > 0) && !px.conv[p]) {
+  uint32_t kn = 0;
+  if (K > 0 && !px.conv[p]) {
+    const double* __restrict__ Lp = L + 3 * (ap.off ? (int64_t)ap.off[q] : p * (int64_t)ap.kuni);
     PixRec r;
     load_pixel(r, px, npix, p);
     const int n0 = r.n;
-    bool blocked = false;
-    const uint32_t pin0 = pk > 0 ? ap.pin_off[q] : 0u;
-    if (pk > 0) {  // the previous record's pending samples: every one has ended since
-      replay_pixel<kRecAhead>(r, L + 3 * (uint64_t)pin0, pk, ap.min_spp, ap.rel, blocked);
-      if (blocked) atomicOr(ap.err, 1ull);
-    }
-    const uint32_t cur0 = ap.lbase + (ap.off ? ap.off[q] : (uint32_t)(p * ap.kuni));
-    int used = 0;
-    if (!r.conv && !blocked && K > 0) {
-      used = replay_pixel<kRecAhead>(r, L + 3 * (uint64_t)cur0, K, ap.min_spp, ap.rel, blocked);
-      if (blocked && !r.conv) po = cur0 + (uint32_t)used, pn = (uint32_t)(K - used);
-    }
+    replay_pixel<kRecAhead>(r, Lp, K, ap.min_spp, ap.rel);
     if (ap.segs) {  // counting render: the segments of the samples recorded (the rest are discarded)
-      const int rec = r.n - n0, from_pin = min(rec, pk);
+      const uint16_t* sg = ap.segs + (ap.off ? (int64_t)ap.off[q] : p * (int64_t)ap.kuni);
       unsigned long long t = 0;
-      for (int k = 0; k < from_pin; k++) t += ap.segs[pin0 + k];
-      for (int k = 0; k < rec - from_pin; k++) t += ap.segs[cur0 + k];
+      for (int k = 0; k < r.n - n0; k++) t += sg[k];
       atomicAdd(ap.rec_segs, t);
     }
     store_pixel(r, px, npix, p);
-    if (!r.conv && r.n + (int)pn < ap.budget) {
-      // A blocked pixel's next batch is predicted from every sample of its batch that has
-      // ended, recorded or not (a prediction needs no order: it only sizes the work), so it is
-      // as good as the drained schedule's; the samples already allocated (recorded + pending)
-      // count against it.
-      PixRec s = r;
-      if (pn > 0 && ap.predict_all) {
-        const double* Lp = L + 3 * (uint64_t)po;
-        for (int k = 1; k < (int)pn; k++) {  // (sample 0 of the pending run is the carried one)
-          const double x0 = Lp[3 * k];
-          if ((uint64_t)__double_as_longlong(x0) == kCarrySentinel) continue;
-          const double x[3] = {x0, Lp[3 * k + 1], Lp[3 * k + 2]};
-          s.n++;
-          for (int c = 0; c < 3; c++) {
-            const double delta = x[c] - s.mean[c];
-            s.mean[c] += delta / s.n;
-            s.m2[c] += (x[c] - s.mean[c]) * delta;
-          }
-        }
-      }
-      const uint32_t alloc = (uint32_t)(s.n - r.n) <= pn ? pn - (uint32_t)(s.n - r.n) : 0u;  // allocated, not in s
-      // a blocked pixel gets more samples only where its prediction asks for more than it has
-      // allocated (no smallest batch: its pending samples are recorded next time anyway)
-      const uint32_t want = adapt_next_batch(s.mean, s.m2, s.n, ap, pn > 0 && ap.predict_all);
-      kn = want > alloc ? min(want - alloc, (uint32_t)(ap.budget - r.n) - pn) : 0u;
-      if (pn > 0 && ap.hold_blocked) kn = 0u;  // (a blocked pixel waits for its pending samples)
-    }
+    if (!r.conv && r.n < ap.budget) kn = adapt_next_batch(r.mean, r.m2, r.n, ap);
   }
   ap.knext[q] = kn;
-  if (ap.pout_k) ap.pout_off[q] = po, ap.pout_k[q] = pn;
   const unsigned long long na = __popcll(__ballot(kn != 0));
   if (na && lane_id() == 0) atomicAdd(ap.next_active, na);
 }
@@ -352,31 +290,23 @@ __global__ __launch_bounds__(kBlock) void k_adapt_record(PixelSoA px, const doub
 // the pixel's budget and the workspace), so a phase with few pixels left is large enough to
 // fill the GPU, and the pixels finish in it rather than in further phases that would be mostly
 // launch drain (the last paths of a launch run with their waves nearly empty).
-// With carried paths: once at most final_px pixels are left, the next phase is the last: every
-// pixel gets the rest of its budget and the launch drains (word kSlotWFinal of the slot counter
-// block, read by k_slot_block_init), instead of a tail of small phases each ending in the
-// latency of its carried-in paths.
 __global__ __launch_bounds__(kBlock) void k_adapt_floor(uint32_t* __restrict__ knext, int64_t nq, int32_t sub_n,
                                                         int32_t sub_j, const int32_t* __restrict__ samples,
-                                                        const uint32_t* __restrict__ pend_k, int32_t budget,
-                                                        int32_t kcap, int64_t target, int64_t final_px,
-                                                        unsigned long long* __restrict__ ctr) {
+                                                        int32_t budget, int32_t kcap, int64_t target,
+                                                        const unsigned long long* __restrict__ next_active) {
   const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const unsigned long long na = ctr[kSlotWCount + 3];  // the next phase's pixel count (k_adapt_record)
-  const bool last = (int64_t)na <= final_px;
-  if (q == 0) ctr[kSlotWFinal] = last ? 1ull : 0ull;
   if (q >= nq) return;
   const uint32_t k = knext[q];
-  // (the last phase: a pixel still waiting for pending samples gets the rest of its budget too)
-  if (k == 0 && !(last && pend_k && pend_k[q] > 0)) return;
-  const int64_t kmin = last ? (int64_t)budget : (target + (int64_t)na - 1) / (int64_t)max(na, 1ull);
-  const int left = budget - samples[q * sub_n + sub_j] - (pend_k ? (int)pend_k[q] : 0);
+  if (k == 0) return;
+  const unsigned long long na = *next_active;
+  const int64_t kmin = (target + (int64_t)na - 1) / (int64_t)max(na, 1ull);
+  const int left = budget - samples[q * sub_n + sub_j];
   int kn = (int)max<int64_t>((int64_t)k, min<int64_t>(kmin, (int64_t)left));
   kn = (kn + 3) & ~3;
   knext[q] = (uint32_t)min(kn, min(left, kcap));
 }
 // The next phase's slot map: sub-pixel q's batch occupies slots [off[q], off[q] + knext[q]),
-// slot off[q] + k being sample samples[p] + pend_k[q] + k of pixel p (after its pending samples).  One block per kExpandPix sub-pixels;
+// slot off[q] + k being sample samples[p] + k of pixel p.  One block per kExpandPix sub-pixels;
 // its slots are a contiguous range written by all its threads (coalesced), each finding its
 // sub-pixel by a search of the block's offsets in LDS.  The last sub-pixel's thread writes the
 // phase's slot count.  (Few pixels per block: the pixels still sampling cluster, and a block
@@ -385,7 +315,6 @@ constexpr int kExpandPix = 32;
 __global__ __launch_bounds__(kBlock) void k_adapt_expand(const uint32_t* __restrict__ knext,
                                                          const uint32_t* __restrict__ off, int64_t nq, int32_t sub_n,
                                                          int32_t sub_j, const int32_t* __restrict__ samples,
-                                                         const uint32_t* __restrict__ pend_k,
                                                          uint2* __restrict__ smap,
                                                          unsigned long long* __restrict__ total) {
   __shared__ uint32_t s_off[kExpandPix], s_p[kExpandPix], s_s0[kExpandPix];
@@ -398,7 +327,7 @@ __global__ __launch_bounds__(kBlock) void k_adapt_expand(const uint32_t* __restr
     const uint32_t k = knext[q], o = off[q];
     const int64_t p = q * sub_n + sub_j;
     act = k != 0;
-    s_off[t] = o, s_p[t] = (uint32_t)p, s_s0[t] = k ? (uint32_t)samples[p] + (pend_k ? pend_k[q] : 0u) : 0u;
+    s_off[t] = o, s_p[t] = (uint32_t)p, s_s0[t] = k ? (uint32_t)samples[p] : 0u;
     if (t == nb - 1) {
       s_end = o + k;
       if (q == nq - 1) total[0] = (unsigned long long)o + k, total[2] = (unsigned long long)smap;
@@ -586,26 +515,16 @@ __global__ __launch_bounds__(kBlock) void k_frame_init(PixelSoA px, int64_t npix
   px.samples[i] = 0;
   px.conv[i] = 0;
 }
-// An adaptive launch's slot counter block (words: rtx_kernels.h, kSlotW*): the 8 region
-// counters and the next phase's pixel count (k_adapt_record's) zeroed; the slot count and slot
-// map set (a.set; else kept as k_adapt_expand wrote them); the radiance base; the carry queues:
-// the previous launch's carry-out count becomes this launch's carry-in count (0 for the first
-// launch), the queues swap, the counters restart.
-struct SlotBlockInit {
-  unsigned long long nslots, smap, lbase, cin, cout, cap, flags;
-  int set, first;
-};
-__global__ void k_slot_block_init(unsigned long long* __restrict__ ctr, SlotBlockInit a) {
+// An adaptive launch's slot counter block: the 8 region counters and the next phase's pixel
+// count (word 8 * 16 + 3, k_adapt_record's) zeroed, the slot count and the slot map's address
+// set (set: 0 keeps them, as k_adapt_expand wrote them).
+__global__ void k_slot_block_init(unsigned long long* __restrict__ ctr, int set, unsigned long long nslots,
+                                  unsigned long long smap) {
   const int i = (int)threadIdx.x;
   if (i < 8 * 16) ctr[i] = 0ull;
   if (i == 0) {
-    ctr[kSlotWCount + 3] = 0ull;
-    if (a.set) ctr[kSlotWCount] = a.nslots, ctr[kSlotWMap] = a.smap;
-    ctr[kSlotWBase] = a.lbase;
-    ctr[kSlotWCinCount] = a.first ? 0ull : ctr[kSlotWCoutCount];
-    ctr[kSlotWCin] = a.cin, ctr[kSlotWCout] = a.cout, ctr[kSlotWCap] = a.cap;
-    ctr[kSlotWFlags] = ctr[kSlotWFinal] ? 0ull : a.flags;  // (the last phase drains, k_adapt_floor)
-    ctr[kSlotWCinClaim] = 0ull, ctr[kSlotWCoutCount] = 0ull;
+    ctr[8 * 16 + 3] = 0ull;
+    if (set) ctr[8 * 16] = nslots, ctr[8 * 16 + 2] = smap;
   }
 }
 __global__ __launch_bounds__(kBlock) void k_resolve(PixelSoA px, int64_t npix, int megakernel, int spp,

@@ -250,41 +250,6 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_wf_extend(RenderArgs A,
 
 
 // ---------------------------------------------------------------------------------------
-// Paths that outlive their launch (adaptive phases, MAP 1).  A phase launch that runs out of
-// slots does not drain: each wave, once the slots are used up, writes its lanes' paths that
-// sit between two segments to a carry queue and leaves; the next launch resumes them before it
-// takes fresh slots.  A carried path's radiance record holds kCarrySentinel until the path
-// ends, so the record after the launch stops a pixel at its first unfinished sample and keeps
-// the rest for the next record (render_adaptive).  A resumed path is never carried again (bit
-// 31 of the lane's slot marks it), so every path carried out of launch g has ended by the end
-// of launch g + 1.  The last launch of a render drains (no carry-out).
-//
-// The slot counter block (next_slot) words the phase launches read, after the 8 region
-// counters (words 0 .. 127, 128 B apart): [128] the phase's slot count, [130] its slot map
-// (0: uniform groups), [132] the counting build's segment buffer, [133] the radiance slot of
-// the phase's local slot 0, [136] / [139] the carry-in / carry-out queue, [137] the carried-in
-// count, [138] the carry-in claim counter, [140] the carry-out counter, [141] the queues'
-// capacity, [142] bit 0: carry-out on (k_slot_block_init sets them before every launch), [143]
-// the next launch is the render's last (k_adapt_floor).
-// ---------------------------------------------------------------------------------------
-constexpr int kSlotWCount = 128, kSlotWMap = 130, kSlotWSegs = 132, kSlotWBase = 133, kSlotWCin = 136,
-              kSlotWCinCount = 137, kSlotWCinClaim = 138, kSlotWCout = 139, kSlotWCoutCount = 140,
-              kSlotWCap = 141, kSlotWFlags = 142, kSlotWFinal = 143;
-constexpr int kSlotBlockWords = 8 * 16 + 16;
-constexpr uint64_t kCarrySentinel = 0x7FF0DEAD0000C0DEull;  // a signalling NaN: no arithmetic result
-constexpr uint32_t kSlotResumed = 0x80000000u;             // lane slot bit: a resumed path (never carried again)
-// A carry queue: SoA over `cap` entries, 9 doubles (origin, direction, throughput) then 5 words
-// (depth, global pixel, sample, radiance slot, counting build's segments so far).
-struct CarryView {
-  double* v;
-  uint32_t* u;
-  uint32_t cap;
-  __device__ __forceinline__ CarryView(unsigned long long base, uint32_t c)
-      : v((double*)base), u((uint32_t*)((double*)base + 9 * (size_t)c)), cap(c) {}
-};
-constexpr size_t carry_queue_bytes(uint32_t cap) { return (size_t)cap * (9 * sizeof(double) + 5 * sizeof(uint32_t)); }
-
-// ---------------------------------------------------------------------------------------
 // Persistent lanes: each lane owns one path at a time and refills from a global slot
 // counter in wave-sized chunks (one atomic per kChunk slots), so lanes whose path ended
 // (miss, emitter, absorption, Russian roulette) are immediately given a new primary —
@@ -334,7 +299,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   // nothing else reads rec.p (textured builds: once the texture lookups moved before the sampling)
   constexpr bool kHitpLds = (NOTEX || kEarlyTex) && !SCATTER;
   (void)hitp_lds;
-  const uint64_t nslots = MAP == 1 ? (uint64_t)next_slot[kSlotWCount] : (uint64_t)A.npix * (uint64_t)A.K;
+  const uint64_t nslots = MAP == 1 ? (uint64_t)next_slot[8 * 16] : (uint64_t)A.npix * (uint64_t)A.K;
   // GetPixel uses Interval(0.001, inf) (camera.h:158); IntersectBatch uses 0.001f (cpu_ray_integrator.h:21)
   const double tmin = SCATTER ? 0.001 : (double)0.001f;
   Counters c{};
@@ -342,13 +307,11 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   // counting builds: the lane's path segments, stored per slot when the launch's slot counter
   // block names a buffer for them (adaptive renders: the segments of the recorded samples)
   uint32_t pseg = 0;
-  uint16_t* const segbuf = !COUNT ? nullptr : (uint16_t*)next_slot[kSlotWSegs];
+  uint16_t* const segbuf = !COUNT ? nullptr : (uint16_t*)next_slot[8 * 16 + 4];
   (void)pseg, (void)segbuf;
   uint64_t chunk_base = 0, chunk_left = 0;  // wave-uniform
   bool exhausted = false;                   // wave-uniform
   bool dry = false;                         // (kShared) wave-uniform: the slot counters are used up
-  constexpr bool kCarry = kShared;          // adaptive phase launches: paths carried across launches
-  bool cin_done = false;                    // (kCarry) wave-uniform: the carry-in queue is used up
   uint32_t region = blockIdx.x & 7;         // wave-uniform
   bool has = false;
   Path P;
@@ -369,7 +332,6 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
     // primary-generation code over several lanes.
     const unsigned long long idle = __ballot(!has);
     bool fresh = false;
-    uint32_t resume = ~0u;  // (kCarry) the carry-in entry this lane resumes
     constexpr int kRefill = kPark ? kRefillMinPark : kRefillMin;
     if (kShared) {
       // block-shared chunks: the wave takes slots from its own chunk word (an LDS add), then from
@@ -381,16 +343,6 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
         const uint32_t rank = (uint32_t)__popcll(idle & ((1ull << lane_id()) - 1ull));
         const int wv = (int)(threadIdx.x >> 6);
         uint32_t given = 0;
-        if (kCarry && !cin_done) {  // the paths carried over from the previous launch first
-          const uint32_t cin = (uint32_t)next_slot[kSlotWCinCount];
-          unsigned long long b = 0;
-          if (lane_id() == 0 && cin) b = atomicAdd(next_slot + kSlotWCinClaim, (unsigned long long)nidle);
-          b = __shfl(b, 0);
-          const uint32_t got = b < cin ? (uint32_t)min<uint64_t>(nidle, cin - b) : 0u;
-          if (!has && rank < got) resume = (uint32_t)b + rank;
-          given = got;
-          if (got < nidle) cin_done = true;
-        }
         auto take = [&](int j) {
           unsigned long long old = 0;
           if (lane_id() == 0) old = atomicAdd(&cw[j], (unsigned long long)(nidle - given));
@@ -471,17 +423,6 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
       }
       if (cand < nslots) slot = (uint32_t)cand, fresh = true;
     }
-    if (kCarry && resume != ~0u) {  // ---- resume a carried path where its last launch left it
-      const CarryView q((unsigned long long)next_slot[kSlotWCin], (uint32_t)next_slot[kSlotWCap]);
-      P.o = v3(q.v[resume], q.v[q.cap + resume], q.v[2 * q.cap + resume]);
-      P.d = v3(q.v[3 * q.cap + resume], q.v[4 * q.cap + resume], q.v[5 * q.cap + resume]);
-      thr_lds[0] = q.v[6 * q.cap + resume], thr_lds[kBlock] = q.v[7 * q.cap + resume];
-      thr_lds[2 * kBlock] = q.v[8 * q.cap + resume];
-      P.depth = (int32_t)q.u[resume], pix = q.u[q.cap + resume], smp = q.u[2 * q.cap + resume];
-      slot = q.u[3 * q.cap + resume] | kSlotResumed;
-      if (COUNT) pseg = q.u[4 * q.cap + resume];
-      has = true;
-    }
     // ---- start the primary path of a freshly assigned slot ----
     if (fresh) {
       // The primary's inputs (camera, pixel map, group) are read from the kernel argument
@@ -503,9 +444,8 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
       // nslots < 2^32 (checked on the host): 32-bit division
       uint2 e = make_uint2(0u, 0u);
       if (MAP == 1) {  // a phase's slot map, or none: uniform groups (the adaptive first pass)
-        const uint2* const sm = (const uint2*)next_slot[kSlotWMap];
+        const uint2* const sm = (const uint2*)next_slot[8 * 16 + 2];
         e = sm ? sm[slot] : make_uint2(slot / (uint32_t)Ar.K, (uint32_t)Ar.s0 + slot % (uint32_t)Ar.K);
-        slot += (uint32_t)next_slot[kSlotWBase];  // the phase's radiance slots
       }
       const uint32_t p = MAP ? e.x : (uint32_t)slot / (uint32_t)Ar.K;
       if (!(Ar.conv && Ar.conv[p])) {
@@ -520,28 +460,6 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
         has = true;
         prims++;
         if (COUNT) pseg = 0;
-      }
-    }
-    if (kCarry && exhausted) {
-      // ---- the slots are used up: carry the paths between two segments over to the next
-      // launch (a parked walk finishes its segment first; a resumed path is not carried again)
-      const bool out = has && !parked && !(slot & kSlotResumed);
-      const unsigned long long m = __ballot(out);
-      if (m != 0 && (next_slot[kSlotWFlags] & 1ull)) {
-        unsigned long long b = 0;
-        if (lane_id() == 0) b = atomicAdd(next_slot + kSlotWCoutCount, (unsigned long long)__popcll(m));
-        b = __shfl(b, 0);
-        const CarryView q((unsigned long long)next_slot[kSlotWCout], (uint32_t)next_slot[kSlotWCap]);
-        const uint64_t i = b + (uint64_t)__popcll(m & ((1ull << lane_id()) - 1ull));
-        if (out && i < q.cap) {  // (beyond the capacity the path runs on here: never reached, the host sizes it)
-          q.v[i] = P.o.x, q.v[q.cap + i] = P.o.y, q.v[2 * q.cap + i] = P.o.z;
-          q.v[3 * q.cap + i] = P.d.x, q.v[4 * q.cap + i] = P.d.y, q.v[5 * q.cap + i] = P.d.z;
-          q.v[6 * q.cap + i] = thr_lds[0], q.v[7 * q.cap + i] = thr_lds[kBlock], q.v[8 * q.cap + i] = thr_lds[2 * kBlock];
-          q.u[i] = (uint32_t)P.depth, q.u[q.cap + i] = pix, q.u[2 * q.cap + i] = smp, q.u[3 * q.cap + i] = slot;
-          q.u[4 * q.cap + i] = COUNT ? pseg : 0u;
-          A.L[3 * (uint64_t)slot] = __longlong_as_double((long long)kCarrySentinel);
-          has = false;
-        }
       }
     }
     if (COUNT && lane_id() == 0) c.witers++;  // (the loop's rounds are wave-uniform: lane 0 counts)
@@ -630,7 +548,6 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
       }
     }
     if (!cont) {
-      if (kCarry) slot &= ~kSlotResumed;
       store_radiance(A, slot, L);
       if (COUNT && segbuf) segbuf[slot] = (uint16_t)min(pseg, 65535u);
       has = false;

@@ -352,25 +352,17 @@ class DeviceScene:
         return st.as_dict() if stats else None
 
 
-def adapt_tune(phase_slots=0, phase_kcap=0, first_map=-1, phase_mstep=-1.0, carry=-1, final_slots=0, carry_until=0,
-               hold_blocked=-1, predict_all=-1):
+def adapt_tune(phase_slots=0, phase_kcap=0, first_map=-1, phase_mstep=-1.0):
     """Test / tuning hook (rtx_internal_adapt_tune, not in rtx.h): overrides of the adaptive
     phases' constants for the renders that follow in this process; no argument restores the
     defaults.  Results never depend on them, only the work and the phases do.  phase_slots: the
     smallest phase while pixels remain; phase_kcap: the largest batch of one pixel; first_map:
     the uniform first pass on the phase kernel (1, block-shared chunks) or on the uniform-group
-    kernel (0; only without carried paths); phase_mstep: the batch margin's growth per phase;
-    carry: 1 phase launches carry their unfinished paths over to the next launch, 0 each one
-    drains; final_slots: with carried paths, the phase after which (pixels left) x (budget -
-    min_spp) is at most this is the last (full budgets, the launch drains); carry_until: only
-    launches 1 .. carry_until carry paths over; hold_blocked: 1 a pixel with pending samples gets
-    no further batch before they are recorded; predict_all: 1 a blocked pixel's next batch is
-    predicted from all its ended samples."""
+    kernel (0); phase_mstep: the batch margin's growth per phase."""
     f = lib().rtx_internal_adapt_tune
-    f.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_double, C.c_int32, C.c_int64, C.c_int32, C.c_int32, C.c_int32]
+    f.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_double]
     f.restype = C.c_int
-    _check(f(phase_slots, phase_kcap, first_map, phase_mstep, carry, final_slots, carry_until, hold_blocked, predict_all),
-           "rtx_internal_adapt_tune")
+    _check(f(phase_slots, phase_kcap, first_map, phase_mstep), "rtx_internal_adapt_tune")
 
 
 def render_multi(scenes, cam, spp, max_depth, seed=1234, adaptive=True, mode="persistent", precision="fast",

@@ -233,19 +233,16 @@ def test_adaptive_schedules_equal_uniform_groups(rtx_mod, dev_scenes, scene, pre
     # (the Cornell box is too noisy for any pixel to converge within 48 samples: every pixel
     # takes the whole budget through the growing batches)
     """Adaptive persistent renders predict each pixel's batches from its statistics: the phase
-    schedule (one launch per phase over a device-wide slot map, unfinished paths carried over to
-    the next launch; also with a forced small workspace and phase floor, with every launch
-    draining instead, and with the uniform first pass on either kernel) gives the same pixels
-    and sample counts, bit for bit, as uniform groups of 4 samples over every pixel."""
+    schedule (one launch per phase over a device-wide slot map; also with a forced small
+    workspace and phase floor, and with the uniform first pass on either kernel) gives the same
+    pixels and sample counts, bit for bit, as uniform groups of 4 samples over every pixel."""
     cam = rtx_mod.camera(rtx_mod.camera_config(preset, width=w))
     d = dev_scenes(scene)
     kw = dict(seed=17, adaptive=True, mode="persistent", precision="fast", schedule=schedule)
     b, sb, stb = d.render(cam, spp, depth, samples_per_group=4, **kw)
     assert sb.min() >= min(16, spp) and sb.max() <= spp and ((sb < spp).any() or scene == "cornell")
     runs = [("phases", {}), ("phases_small", dict(phase_slots=1024, phase_kcap=8)),
-            ("phases_tiny_carry", dict(phase_slots=64, phase_kcap=4)),
-            ("phases_drain", dict(carry=0)), ("phases_drain_first_uniform", dict(carry=0, first_map=0)),
-            ("phases_wide_margin", dict(phase_mstep=1.5))]
+            ("phases_first_uniform", dict(first_map=0)), ("phases_wide_margin", dict(phase_mstep=1.5))]
     try:
         for name, tune in runs:
             rtx_mod.adapt_tune(**tune)
