@@ -151,7 +151,7 @@ static double host_us() {
 }
 static thread_local double g_t_launch = 0, g_t_sync0 = 0, g_t_sync1 = 0;
 struct AdaptWs {
-  DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer
+  DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer, then the spread pixel counts (kSpreadBase)
   DevBuf segs;                                  // counting renders: each slot's path segments (u16)
   HostBuf total_h;                              // pinned copy of the next phase's slot count
   hipEvent_t ev = nullptr;                      // total_h written
@@ -761,7 +761,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     for (DevBuf* b : {&w.k[0], &w.k[1], &w.off})
       if ((rc = b->reserve(npix * sizeof(uint32_t)))) return rc;
     if ((rc = w.scan_tmp.reserve(std::max<size_t>(16, rtxscan::temp_bytes(npix))))) return rc;
-    if ((rc = w.ctr.reserve(8 * 16 * sizeof(unsigned long long) + 64))) return rc;
+    if ((rc = w.ctr.reserve(kAdaptCtrWords * sizeof(unsigned long long)))) return rc;
     if ((rc = w.total_h.reserve(2 * sizeof(unsigned long long)))) return rc;
     if (!w.ev) HIPC(hipEventCreateWithFlags(&w.ev, hipEventDisableTiming));
   }
@@ -783,13 +783,12 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ap.margin_step = g_tune.phase_mstep >= 0 ? g_tune.phase_mstep : kAdaptMarginStep;
     ap.segs = !L.count ? nullptr : g == 1 ? sc->segs1.as<uint16_t>() : w.segs.as<uint16_t>();
     ap.rec_segs = A.counters + 9;
-    ap.active = ctr + 8 * 16 + 1;
-    ap.next_active = ctr + 8 * 16 + 3;
+    ap.next_active = ctr + kSpreadBase;
     // (ap.next_active was zeroed with the phase's slot counter block, k_slot_block_init)
-    hipLaunchKernelGGL(k_adapt_record, dim3(qb), dim3(kBlock), 0, s, px, Lph, npix, npix, ap);
+    hipLaunchKernelGGL(k_adapt_record, dim3((unsigned)((npix + 63) / 64)), dim3(64), 0, s, px, Lph, npix, npix, ap);
     HIPC(hipGetLastError());
     hipLaunchKernelGGL(k_adapt_floor, dim3(qb), dim3(kBlock), 0, s, ap.knext, npix, 1, 0, (const int32_t*)px.samples,
-                       budget, kcap, phase_slots, (const unsigned long long*)ap.next_active);
+                       budget, kcap, phase_slots, (const unsigned long long*)ap.next_active, ctr + 8 * 16 + 1);
     HIPC(hipGetLastError());
     HIPC(rtxscan::exclusive_scan_u32(ap.knext, w.off.as<uint32_t>(), npix, w.scan_tmp.p, w.scan_tmp.n, s));
     hipLaunchKernelGGL(k_adapt_expand, dim3((unsigned)((npix + kExpandPix - 1) / kExpandPix)), dim3(kBlock), 0, s,

@@ -88,69 +88,49 @@ __global__ __launch_bounds__(kBlock) void k_wf_shade(RenderArgs A, PathQueue in,
 }
 
 // ---------------------------------------------------------------------------------------
-// One pixel's RecordSample (pixel_state.h:22-39) over K radiance records in sample order, each
-// followed by IsConverged (pixel_state.h:54-72), stopping at convergence; the statistics come
-// in and go out through r.  AHEAD: the loads of the next samples kept in flight while the
-// current one is replayed (k_adapt_record).
+// One radiance record x of a pixel: RecordSample (pixel_state.h:22-39), then IsConverged
+// (pixel_state.h:54-72) once the pixel has min_spp samples; the statistics come in and go out
+// through r (k_adapt_record).
 // ---------------------------------------------------------------------------------------
 struct PixRec {
   double sum[3], mean[3], m2[3];
   int n;
   bool conv;
 };
-template <int AHEAD>
-__device__ __forceinline__ void replay_pixel(PixRec& r, const double* __restrict__ Lp, int K, int min_spp,
-                                             double rel) {
-  auto record = [&](const double (&x)[3]) {
-    r.n++;
-    for (int c = 0; c < 3; c++) {
-      double mu = r.mean[c];
-      double delta = x[c] - mu;
-      mu += delta / r.n;
-      double delta2 = x[c] - mu;
-      r.mean[c] = mu;
-      r.m2[c] += delta2 * delta;
-    }
-    for (int c = 0; c < 3; c++) r.sum[c] += x[c];
-    if (r.n >= min_spp) {
-      // err / mu > rel  <=>  m2 > rel^2 (n - 1) n mu^2 up to the few ulps the exact form rounds
-      // by: decided by products where the two sides differ by more than 1e-10 relative (the
-      // usual case), the exact form (two divisions, two square roots) only in between; NaN
-      // fails both comparisons and takes the exact form too.
-      // (channels in order, the first failing one decides; unrolled, so the statistics stay in
-      // registers)
-      bool ok = true;
+__device__ __forceinline__ void record_sample(PixRec& r, const double (&x)[3], int min_spp, double rel) {
+  r.n++;
+  for (int c = 0; c < 3; c++) {
+    double mu = r.mean[c];
+    double delta = x[c] - mu;
+    mu += delta / r.n;
+    double delta2 = x[c] - mu;
+    r.mean[c] = mu;
+    r.m2[c] += delta2 * delta;
+  }
+  for (int c = 0; c < 3; c++) r.sum[c] += x[c];
+  if (r.n >= min_spp) {
+    // err / mu > rel  <=>  m2 > rel^2 (n - 1) n mu^2 up to the few ulps the exact form rounds
+    // by: decided by products where the two sides differ by more than 1e-10 relative (the
+    // usual case), the exact form (two divisions, two square roots) only in between; NaN
+    // fails both comparisons and takes the exact form too.
+    // (channels in order, the first failing one decides; unrolled, so the statistics stay in
+    // registers)
+    bool ok = true;
 #pragma unroll
-      for (int c = 0; c < 3; c++) {
-        if (ok) {
-          double mu = fmax(fabs(r.mean[c]), 1e-3);
-          const double thr = rel * rel * ((double)(r.n - 1) * (double)r.n * (mu * mu));
-          if (r.m2[c] > thr * (1.0 + 1e-10)) {
-            ok = false;
-          } else if (!(r.m2[c] < thr * (1.0 - 1e-10))) {
-            double var = r.n > 1 ? r.m2[c] / (r.n - 1) : 0.0;
-            double err = sqrt(var) / sqrt((double)r.n);
-            if (err / mu > rel) ok = false;
-          }
+    for (int c = 0; c < 3; c++) {
+      if (ok) {
+        double mu = fmax(fabs(r.mean[c]), 1e-3);
+        const double thr = rel * rel * ((double)(r.n - 1) * (double)r.n * (mu * mu));
+        if (r.m2[c] > thr * (1.0 + 1e-10)) {
+          ok = false;
+        } else if (!(r.m2[c] < thr * (1.0 - 1e-10))) {
+          double var = r.n > 1 ? r.m2[c] / (r.n - 1) : 0.0;
+          double err = sqrt(var) / sqrt((double)r.n);
+          if (err / mu > rel) ok = false;
         }
       }
-      r.conv = ok;
     }
-  };
-  double b[AHEAD][3];
-  auto load = [&](int slot, int k) {
-    if (k < K)
-      for (int c = 0; c < 3; c++) b[slot][c] = Lp[3 * k + c];
-  };
-#pragma unroll
-  for (int i = 0; i < AHEAD; i++) load(i, i);
-  for (int k = 0; k < K && !r.conv; k += AHEAD) {
-#pragma unroll
-    for (int i = 0; i < AHEAD; i++) {
-      if (k + i >= K || r.conv) break;
-      record(b[i]);
-      load(i, k + i + AHEAD);
-    }
+    r.conv = ok;
   }
 }
 __device__ __forceinline__ void load_pixel(PixRec& r, const PixelSoA& px, int64_t npix, int64_t p) {
@@ -235,8 +215,8 @@ struct AdaptPlan {
   double margin_step;  // the batch margin grows by this much per phase (1 + step * (phase - 1))
   const uint16_t* segs;           // counting renders: segments of each slot's path (else nullptr)
   unsigned long long* rec_segs;   // ... summed here over the samples the pixels record
-  unsigned long long* active;  // the next phase's pixel count (k_adapt_expand adds; zeroed here)
-  unsigned long long* next_active;  // ... counted here too (zeroed before the launch), for k_adapt_floor
+  unsigned long long* next_active;  // the next phase's pixel count, in kSpread words kSpreadStride
+                                    // apart (added here, zeroed before the launch; k_adapt_floor sums)
 };
 __device__ __forceinline__ uint32_t adapt_next_batch(const double (&mean)[3], const double (&m2)[3], int n,
                                                      const AdaptPlan& ap) {
@@ -254,27 +234,93 @@ __device__ __forceinline__ uint32_t adapt_next_batch(const double (&mean)[3], co
   k = (k + 3) & ~3;
   return (uint32_t)min(k, min(left, ap.kcap));
 }
-// One lane per sub-pixel: the replay of a pixel's samples is sequential (each step divides by
-// the running count), so the parallelism is across pixels, and each lane streams its own run
-// of the phase's slots with the loads of the next kRecAhead samples in flight while it
-// replays the current one (a lane's run is contiguous: its loads walk the same cache lines).
-constexpr int kRecAhead = 8;  // (16: -0.5 %, 32: -2.3 %: occupancy, ab_rec_ahead_r6a_c3a.txt)
-__global__ __launch_bounds__(kBlock) void k_adapt_record(PixelSoA px, const double* __restrict__ L, int64_t nq,
-                                                         int64_t npix, AdaptPlan ap) {
-  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (q == 0) *ap.active = 0;  // k_adapt_expand, later on the stream, counts the next phase's pixels
-  if (q >= nq) return;
-  const int64_t p = q * ap.sub_n + ap.sub_j;
-  const int K = ap.kcur ? (int)ap.kcur[q] : ap.kuni;
+// Counters that every wave of a launch adds to are spread over kSpread words kSpreadStride words
+// apart (a device-scope atomic add to one word serialises at ~10 ns per wave)
+constexpr int kSpread = 64, kSpreadStride = 16;
+// One lane per sub-pixel, one wave per block: the replay of a pixel's samples is sequential
+// (each step divides by the running count), so the parallelism is across pixels.  The wave's
+// 64 runs of the phase's radiance records (each contiguous: pixel-major slots) come in windows
+// of kRecWin samples per lane, transposed through LDS: in each load instruction, 8 lanes read 8
+// consecutive 8-byte pieces of one run, so an instruction touches 8 runs (~12 cache lines)
+// instead of 64; each lane then replays its own run from LDS.  The next window's loads are in
+// flight while the current one is replayed.
+#ifndef RTX_REC_WIN
+#define RTX_REC_WIN 8
+#endif
+constexpr int kRecWin = RTX_REC_WIN, kRecPieces = 3 * kRecWin,
+              kRecPitch = kRecPieces + 1,  // (odd pitch: a lane's row starts on another bank)
+    kRecLpr = 8,                           // lanes per run in a load instruction
+    kRecRuns = 64 / kRecLpr,               // runs per load instruction
+    kRecGroups = (kRecPieces + kRecLpr - 1) / kRecLpr;  // load instructions per run and window
+__global__ __launch_bounds__(64) void k_adapt_record(PixelSoA px, const double* __restrict__ L, int64_t nq,
+                                                     int64_t npix, AdaptPlan ap) {
+  __shared__ double s_win[64 * kRecPitch];
+  __shared__ int64_t s_base[64];  // the lane's first radiance word
+  __shared__ int32_t s_n[64];     // its words in the window being fetched
+  const int lane = (int)threadIdx.x;
+  const int64_t q = (int64_t)blockIdx.x * 64 + lane;
+  int64_t p = 0, base = 0;
+  int K = 0;
+  bool act = false;
+  PixRec r;
+  r.n = 0, r.conv = false;
+  if (q < nq) {
+    p = q * ap.sub_n + ap.sub_j;
+    K = ap.kcur ? (int)ap.kcur[q] : ap.kuni;
+    act = K > 0 && !px.conv[p];
+    base = 3 * (ap.off ? (int64_t)ap.off[q] : p * (int64_t)ap.kuni);
+    if (act) load_pixel(r, px, npix, p);
+  }
+  const int n0 = r.n;
+  s_base[lane] = base;
+  s_n[lane] = act ? 3 * min(K, kRecWin) : 0;
+  __syncthreads();
+  // this lane's part of the loads: runs kRecRuns * j + a, pieces kRecLpr * g + b of each
+  const int a = lane / kRecLpr, b = lane % kRecLpr;
+  const double* rp[kRecRuns];
+#pragma unroll
+  for (int j = 0; j < kRecRuns; j++) rp[j] = L + s_base[kRecRuns * j + a] + b;
+  double v[kRecRuns * kRecGroups];
+  uint32_t got = 0;
+  static_assert(kRecRuns * kRecGroups <= 32, "got: one bit per load");
+  auto fetch = [&](int t) {  // the window of samples [t, t + kRecWin) of every lane's run
+    got = 0;
+#pragma unroll
+    for (int j = 0; j < kRecRuns; j++) {
+      const int nj = s_n[kRecRuns * j + a];
+#pragma unroll
+      for (int g = 0; g < kRecGroups; g++)
+        if (kRecLpr * g + b < nj) v[j * kRecGroups + g] = rp[j][3 * t + kRecLpr * g], got |= 1u << (j * kRecGroups + g);
+    }
+  };
+  fetch(0);
+  for (int t = 0;; t += kRecWin) {
+    __syncthreads();  // the previous window is replayed, s_n read
+#pragma unroll
+    for (int j = 0; j < kRecRuns; j++)
+#pragma unroll
+      for (int g = 0; g < kRecGroups; g++)
+        if (got >> (j * kRecGroups + g) & 1)
+          s_win[(kRecRuns * j + a) * kRecPitch + kRecLpr * g + b] = v[j * kRecGroups + g];
+    const int nn = act && !r.conv ? 3 * max(0, min(K - t - kRecWin, kRecWin)) : 0;
+    s_n[lane] = nn;
+    __syncthreads();
+    const bool more = __ballot(nn > 0) != 0ull;
+    if (more) fetch(t + kRecWin);
+    if (act && !r.conv) {
+      const double* w = s_win + lane * kRecPitch;
+      const int c = min(K - t, kRecWin);
+      for (int k = 0; k < c && !r.conv; k++) {
+        const double x[3] = {w[3 * k], w[3 * k + 1], w[3 * k + 2]};
+        record_sample(r, x, ap.min_spp, ap.rel);
+      }
+    }
+    if (!more) break;
+  }
   uint32_t kn = 0;
-  if (K > 0 && !px.conv[p]) {
-    const double* __restrict__ Lp = L + 3 * (ap.off ? (int64_t)ap.off[q] : p * (int64_t)ap.kuni);
-    PixRec r;
-    load_pixel(r, px, npix, p);
-    const int n0 = r.n;
-    replay_pixel<kRecAhead>(r, Lp, K, ap.min_spp, ap.rel);
+  if (act) {
     if (ap.segs) {  // counting render: the segments of the samples recorded (the rest are discarded)
-      const uint16_t* sg = ap.segs + (ap.off ? (int64_t)ap.off[q] : p * (int64_t)ap.kuni);
+      const uint16_t* sg = ap.segs + base / 3;
       unsigned long long t = 0;
       for (int k = 0; k < r.n - n0; k++) t += sg[k];
       atomicAdd(ap.rec_segs, t);
@@ -282,23 +328,28 @@ __global__ __launch_bounds__(kBlock) void k_adapt_record(PixelSoA px, const doub
     store_pixel(r, px, npix, p);
     if (!r.conv && r.n < ap.budget) kn = adapt_next_batch(r.mean, r.m2, r.n, ap);
   }
-  ap.knext[q] = kn;
+  if (q < nq) ap.knext[q] = kn;
   const unsigned long long na = __popcll(__ballot(kn != 0));
-  if (na && lane_id() == 0) atomicAdd(ap.next_active, na);
+  if (na && lane == 0) atomicAdd(ap.next_active + (blockIdx.x % kSpread) * kSpreadStride, na);
 }
 // Once the next phase's pixel count is known: every batch at least target / that count (within
 // the pixel's budget and the workspace), so a phase with few pixels left is large enough to
 // fill the GPU, and the pixels finish in it rather than in further phases that would be mostly
 // launch drain (the last paths of a launch run with their waves nearly empty).
+// It also writes that count (the next phase's pixels) for the host (*pixels).
 __global__ __launch_bounds__(kBlock) void k_adapt_floor(uint32_t* __restrict__ knext, int64_t nq, int32_t sub_n,
                                                         int32_t sub_j, const int32_t* __restrict__ samples,
                                                         int32_t budget, int32_t kcap, int64_t target,
-                                                        const unsigned long long* __restrict__ next_active) {
+                                                        const unsigned long long* __restrict__ next_active,
+                                                        unsigned long long* __restrict__ pixels) {
   const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  static_assert(kSpread == 64, "one spread counter per lane");
+  unsigned long long na = next_active[lane_id() * kSpreadStride];
+  for (int m = 32; m >= 1; m >>= 1) na += (unsigned long long)__shfl_xor((long long)na, m);
+  if (q == 0) *pixels = na;
   if (q >= nq) return;
   const uint32_t k = knext[q];
   if (k == 0) return;
-  const unsigned long long na = *next_active;
   const int64_t kmin = (target + (int64_t)na - 1) / (int64_t)max(na, 1ull);
   const int left = budget - samples[q * sub_n + sub_j];
   int kn = (int)max<int64_t>((int64_t)k, min<int64_t>(kmin, (int64_t)left));
@@ -309,7 +360,7 @@ __global__ __launch_bounds__(kBlock) void k_adapt_floor(uint32_t* __restrict__ k
 // slot off[q] + k being sample samples[p] + k of pixel p.  One block per kExpandPix sub-pixels;
 // its slots are a contiguous range written by all its threads (coalesced), each finding its
 // sub-pixel by a search of the block's offsets in LDS.  The last sub-pixel's thread writes the
-// phase's slot count.  (Few pixels per block: the pixels still sampling cluster, and a block
+// phase's slot count and the map's address (k_adapt_floor wrote its pixel count).  (Few pixels per block: the pixels still sampling cluster, and a block
 // over 256 of them had up to 256 x kcap slots to write while most blocks had none.)
 constexpr int kExpandPix = 32;
 __global__ __launch_bounds__(kBlock) void k_adapt_expand(const uint32_t* __restrict__ knext,
@@ -322,19 +373,15 @@ __global__ __launch_bounds__(kBlock) void k_adapt_expand(const uint32_t* __restr
   const int t = threadIdx.x;
   const int64_t q0 = (int64_t)blockIdx.x * kExpandPix, q = q0 + t;
   const int nb = (int)min<int64_t>(kExpandPix, nq - q0);
-  bool act = false;
   if (t < nb) {
     const uint32_t k = knext[q], o = off[q];
     const int64_t p = q * sub_n + sub_j;
-    act = k != 0;
     s_off[t] = o, s_p[t] = (uint32_t)p, s_s0[t] = k ? (uint32_t)samples[p] : 0u;
     if (t == nb - 1) {
       s_end = o + k;
       if (q == nq - 1) total[0] = (unsigned long long)o + k, total[2] = (unsigned long long)smap;
     }
   }
-  const unsigned long long nact = __popcll(__ballot(act));  // total[1]: the phase's pixels
-  if (nact && lane_id() == 0) atomicAdd(total + 1, nact);
   __syncthreads();
   const uint32_t b = s_off[0], e = s_end;
   for (uint32_t i = b + t; i < e; i += kBlock) {
@@ -515,17 +562,17 @@ __global__ __launch_bounds__(kBlock) void k_frame_init(PixelSoA px, int64_t npix
   px.samples[i] = 0;
   px.conv[i] = 0;
 }
-// An adaptive launch's slot counter block: the 8 region counters and the next phase's pixel
-// count (word 8 * 16 + 3, k_adapt_record's) zeroed, the slot count and the slot map's address
+// An adaptive launch's slot counter block: the 8 region counters and the next phase's spread
+// pixel counts (kSpreadBase, k_adapt_record's) zeroed, the slot count and the slot map's address
 // set (set: 0 keeps them, as k_adapt_expand wrote them).
+constexpr int kSpreadBase = 8 * 16 + 16;  // (words; the slot block is words 8 * 16 .. + 4)
+constexpr int kAdaptCtrWords = kSpreadBase + kSpread * kSpreadStride;
 __global__ void k_slot_block_init(unsigned long long* __restrict__ ctr, int set, unsigned long long nslots,
                                   unsigned long long smap) {
   const int i = (int)threadIdx.x;
   if (i < 8 * 16) ctr[i] = 0ull;
-  if (i == 0) {
-    ctr[8 * 16 + 3] = 0ull;
-    if (set) ctr[8 * 16] = nslots, ctr[8 * 16 + 2] = smap;
-  }
+  if (i < kSpread) ctr[kSpreadBase + i * kSpreadStride] = 0ull;
+  if (i == 0 && set) ctr[8 * 16] = nslots, ctr[8 * 16 + 2] = smap;
 }
 __global__ __launch_bounds__(kBlock) void k_resolve(PixelSoA px, int64_t npix, int megakernel, int spp,
                                                     double* __restrict__ rgb, int32_t* __restrict__ spp_out) {

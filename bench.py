@@ -550,7 +550,7 @@ def cpu_reference(host, preset, width, spp, depth, args):
 
         probe = run(1)
         n = int(max(1, min(spp, 10.0 / max(float(probe["loop_seconds"]), 1e-3))))
-        st = run(n)
+        st = run(n) if n > 1 else probe  # (4K frames: the 1-spp probe alone is ~10-20 s)
     rays, sec = int(st["rays"]), float(st["loop_seconds"])
     return {"value": rays / sec / 1e6, "unit": "Mrays/s", "cores": threads, "nproc": os.cpu_count(), "kind": "reference",
             "sample": f"the whole {width}-wide frame at {n} spp (of {spp}), depth {depth}, fixed spp: {rays} segments "

@@ -1424,6 +1424,58 @@ int orc_render_var(void* sp, orc_camera* c, const orc_params* p, double* fb, int
 int orc_render(void* sp, orc_camera* c, const orc_params* p, double* fb, int* spp, long long* stats) {
   return orc_render_var(sp, c, p, fb, spp, stats, nullptr);
 }
+// Every sample of every pixel of the tile at fixed spp, philox per-pixel order: radiance in
+// L[3 * (pixel * spp + s)], path segments in segs[pixel * spp + s].  Input of the adaptive
+// schedule simulator (scripts/adaptive_sim.py), which replays RecordSample / IsConverged and the
+// phase policy over these samples without a GPU.
+int orc_render_samples(void* sp, orc_camera* c, const orc_params* p, double* L, unsigned short* segs) {
+  Scene* s = (Scene*)sp;
+  Camera cam;
+  cam.aspect = c->aspect, cam.vfov = c->vfov, cam.defocus = c->defocus, cam.focus = c->focus;
+  cam.width = c->width;
+  cam.lookfrom = v3(c->lookfrom[0], c->lookfrom[1], c->lookfrom[2]);
+  cam.lookat = v3(c->lookat[0], c->lookat[1], c->lookat[2]);
+  cam.vup = v3(c->vup[0], c->vup[1], c->vup[2]);
+  cam.init();
+  c->height = cam.height;
+  Params P;
+  P.spp = p->spp, P.max_depth = p->max_depth, P.adaptive = 0, P.rng_mode = 1;
+  P.seed = p->seed, P.threads = p->threads > 0 ? p->threads : 1;
+  P.x0 = p->x0, P.y0 = p->y0, P.w = p->w > 0 ? p->w : cam.width, P.h = p->h > 0 ? p->h : cam.height;
+  if (P.x0 < 0 || P.y0 < 0 || P.x0 + P.w > cam.width || P.y0 + P.h > cam.height) {
+    g_err = "tile outside image";
+    return -1;
+  }
+  const Scene& S = *s;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(P.threads)
+  for (int ty = 0; ty < P.h; ty++) {
+    for (int tx = 0; tx < P.w; tx++) {
+      const int x = P.x0 + tx, y = P.y0 + ty;
+      const size_t o = (size_t)ty * P.w + tx;
+      Rng g;
+      g.mode = 1, g.seed = P.seed, g.pixel = y * cam.width + x;
+      for (int smp = 0; smp < P.spp; smp++) {
+        g.sample = smp, g.open(0);
+        PathState path;
+        cam.get_ray(x, y, g, path.o, path.d);
+        unsigned n = 0;
+        while (true) {
+          Hit rec;
+          bool hit = S.hit(path.o, path.d, (double)0.001f, kInf, rec);
+          n++;
+          V3 Lr;
+          if (!shade(S, P, path, rec, hit, g, Lr)) {
+            const size_t k = o * P.spp + smp;
+            L[3 * k] = Lr.x, L[3 * k + 1] = Lr.y, L[3 * k + 2] = Lr.z;
+            segs[k] = (unsigned short)(n > 65535 ? 65535 : n);
+            break;
+          }
+        }
+      }
+    }
+  }
+  return 0;
+}
 // Philox stream check for the GPU RNG: out[i] = RandomDouble for (seed, pixel, sample,
 // stream, draw = i)
 int orc_philox_stream(unsigned long long seed, unsigned pixel, unsigned sample, unsigned stream, int n,

@@ -49,7 +49,7 @@ def main():
         out[k] = {"launches": n, **v}
     json.dump(out, open(os.path.join(prof, f"pmc_{tag}.json"), "w"), indent=1, sort_keys=True)
     if adaptive:
-        adaptive_profile(d, out, rnd, tag, workload, mode, prec)
+        adaptive_profile(d, out, launches, rnd, tag, workload, mode, prec)
         return
     # non-counting instantiation of the hot kernel (k_persistent<STACK, FAST, COUNT, SCATTER, PARK>:
     # either schedule; the one with the most wave cycles is the frame kernel)
@@ -121,8 +121,10 @@ def valu_profile(d, k, v, launches, hbm_per_launch, rnd, tag, workload, mode, pr
     print(json.dumps(out))
 
 
-def adaptive_profile(d, out, rnd, tag, workload, mode, prec):
-    """Sums over the frame kernels (non-counting k_persistent launches, every phase) per segment."""
+def adaptive_profile(d, out, launches, rnd, tag, workload, mode, prec):
+    """Sums over the frame kernels (non-counting k_persistent launches, every phase) per segment;
+    the counters also per launch (averaged over the phase launches of the profiled frames, every
+    PMC pass running the same frames), so bench.py prices the adaptive mix as it does a fixed one."""
     ks = [k for k in out if k.startswith("void rtxd::k_persistent<") and ", true, false, false," in k]
 
     def total(c):
@@ -144,6 +146,18 @@ def adaptive_profile(d, out, rnd, tag, workload, mode, prec):
            "valu_insts_per_segment": insts / segs_valu, "lane_ops_per_segment": insts * 64 * util / segs_valu,
            "hbm_bytes_per_segment": hbm, "source": f"profiles/{rnd}/pmc_{tag}.json",
            "formula": "sums over every phase launch of the frame kernels / segments of the profiled frames"}
+
+    def nl(c):
+        return max(1, sum(len(launches[(k, c)]) for k in ks))
+
+    n_valu = nl("SQ_INSTS_VALU")
+    res.update({"segments_per_launch": segs_valu / n_valu, "valu_insts_per_launch": insts / n_valu,
+                "active_inst_valu_per_launch": total("SQ_ACTIVE_INST_VALU") / nl("SQ_ACTIVE_INST_VALU")})
+    for c in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64",
+              "SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_TRANS_F64", "SQ_ACTIVE_INST_VALU2", "SQ_INSTS_VALU_TRANS_F32",
+              "SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_CVT", "SQ_INSTS_VALU_FMA_F32"):
+        if any(c in out[k] for k in ks):
+            res[c.lower() + "_per_launch"] = total(c) / nl(c)
     json.dump(res, open(os.path.join(ROOT, "profiles", f"valu_{workload}_{mode}_{prec}_adaptive.json"), "w"),
               indent=1)
     print(json.dumps(res))

@@ -57,6 +57,8 @@ def lib():
                                  C.c_void_p]
         L.orc_render_var.argtypes = [C.c_void_p, C.POINTER(OrcCamera), C.POINTER(OrcParams), C.c_void_p,
                                      C.c_void_p, C.c_void_p, C.c_void_p]
+        L.orc_render_samples.argtypes = [C.c_void_p, C.POINTER(OrcCamera), C.POINTER(OrcParams), C.c_void_p,
+                                         C.c_void_p]
         L.orc_philox.argtypes = [C.c_ulonglong, C.c_uint, C.c_uint, C.c_int, C.c_void_p]
         L.orc_philox_stream.argtypes = [C.c_ulonglong, C.c_uint, C.c_uint, C.c_uint, C.c_int, C.c_void_p]
         L.orc_write_ppm.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_char_p]
@@ -159,6 +161,22 @@ class Scene:
         if variance:  # per-pixel sample variance m2/(n-1) (pixel_state.h:41-49)
             st["variance"] = var
         return fb, spp_out, st
+
+    def render_samples(self, cam_cfg, width, spp, max_depth, seed, tile=None, threads=1):
+        """Every sample of every pixel at fixed spp (philox, per-pixel order): radiance
+        [h, w, spp, 3] and path segments [h, w, spp] (scripts/adaptive_sim.py)."""
+        cam = make_camera(cam_cfg, width)
+        p = OrcParams()
+        p.spp, p.max_depth, p.adaptive, p.rng_mode, p.seed, p.threads, p.mode = spp, max_depth, 0, 1, seed, threads, 1
+        if tile is None:
+            tile = (0, 0, cam.width, cam.height)
+        p.x0, p.y0, p.w, p.h = tile
+        w, h = tile[2], tile[3]
+        L = np.zeros((h, w, spp, 3))
+        segs = np.zeros((h, w, spp), np.uint16)
+        if lib().orc_render_samples(self.h, C.byref(cam), C.byref(p), _ptr(L), _ptr(segs)) != 0:
+            raise RuntimeError(lib().orc_last_error().decode())
+        return L, segs
 
 
 def aabb(cases):
