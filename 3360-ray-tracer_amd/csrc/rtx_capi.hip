@@ -130,7 +130,9 @@ struct BandSink {
 constexpr int kBands = 8;  // bands of the last accumulate and of the D2H copies that overlap them (ab_bands_*: 2 / 4 / 8 / 16)
 
 // Adaptive renders in phases (render_adaptive)
-constexpr int64_t kAdaptPhaseSlots = 1 << 23;  // render_adaptive: smallest phase planned while pixels remain (ab r3x/r3y: 2^21..2^25)
+// render_adaptive: the smallest phase planned while pixels remain (r05 r8d / r8e: 2^20 +0.8-1.0 %
+// against round 3's 2^23 on C3 adaptive; scripts/adaptive_sim.py ranks the floors offline)
+constexpr int64_t kAdaptPhaseSlots = 1 << 20;
 constexpr double kAdaptMarginStep = 0.25;      // render_adaptive: batch margin 1 + step * (phase - 1) (0.5: within noise, r3y)
 // Overrides of the adaptive schedules' constants (0: the default): rtx_internal_adapt_tune, a
 // test and tuning hook (not in rtx.h) that forces small workspaces and floors, so the paths
@@ -151,12 +153,15 @@ static double host_us() {
 }
 static thread_local double g_t_launch = 0, g_t_sync0 = 0, g_t_sync1 = 0;
 struct AdaptWs {
-  DevBuf lbuf, smap, k[2], off, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer, then the spread pixel counts (kSpreadBase)
+  // lst / kl / ol: the phases' pixel lists (ping-pong: sub-pixel, samples, first slot per entry);
+  // knext: the next batch per entry of the phase just traced; pk: their packed prefix sums
+  DevBuf lbuf, smap, lst[2], kl[2], ol[2], knext, pk, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer, then the spread pixel counts (kSpreadBase)
   DevBuf segs;                                  // counting renders: each slot's path segments (u16)
   HostBuf total_h;                              // pinned copy of the next phase's slot count
   hipEvent_t ev = nullptr;                      // total_h written
   void release() {
-    for (DevBuf* b : {&lbuf, &smap, &k[0], &k[1], &off, &scan_tmp, &ctr, &segs})
+    for (DevBuf* b : {&lbuf, &smap, &lst[0], &lst[1], &kl[0], &kl[1], &ol[0], &ol[1], &knext, &pk, &scan_tmp, &ctr,
+                      &segs})
       b->release();
     total_h.release();
     if (ev) (void)hipEventDestroy(ev);
@@ -758,22 +763,24 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     if ((rc = w.lbuf.reserve(slots * 3 * sizeof(double)))) return rc;
     if (L.count && (rc = w.segs.reserve(slots * sizeof(uint16_t)))) return rc;
     if ((rc = w.smap.reserve(slots * sizeof(uint2)))) return rc;
-    for (DevBuf* b : {&w.k[0], &w.k[1], &w.off})
+    for (DevBuf* b : {&w.lst[0], &w.lst[1], &w.kl[0], &w.kl[1], &w.ol[0], &w.ol[1], &w.knext})
       if ((rc = b->reserve(npix * sizeof(uint32_t)))) return rc;
-    if ((rc = w.scan_tmp.reserve(std::max<size_t>(16, rtxscan::temp_bytes(npix))))) return rc;
+    if ((rc = w.pk.reserve(npix * sizeof(unsigned long long)))) return rc;
+    if ((rc = w.scan_tmp.reserve(std::max<size_t>(16, rtxscan::temp_bytes_packed(npix))))) return rc;
     if ((rc = w.ctr.reserve(kAdaptCtrWords * sizeof(unsigned long long)))) return rc;
     if ((rc = w.total_h.reserve(2 * sizeof(unsigned long long)))) return rc;
     if (!w.ev) HIPC(hipEventCreateWithFlags(&w.ev, hipEventDisableTiming));
   }
   unsigned long long* ctr = w.ctr.as<unsigned long long>();  // 8 region counters, then the slot count, ...
-  const unsigned qb = (unsigned)((npix + kBlock - 1) / kBlock);
   // record + next batch sizes after phase g (its slots in Lph: the uniform first phase's, or the
-  // phase's slot map), then the next phase's prefix sum, slot map and (to the host) slot count
+  // phase's slot map; its `active` pixels in its list), then the next phase's prefix sum, slot
+  // map, pixel list and (to the host) slot and pixel counts
   auto record = [&](int g, const double* Lph, int64_t active) -> int {
     AdaptPlan ap;
-    ap.kcur = g == 1 ? nullptr : w.k[g & 1].as<uint32_t>();
-    ap.off = g == 1 ? nullptr : w.off.as<uint32_t>();
-    ap.knext = w.k[(g + 1) & 1].as<uint32_t>();
+    ap.list = g == 1 ? nullptr : w.lst[g & 1].as<uint32_t>();
+    ap.kcur = g == 1 ? nullptr : w.kl[g & 1].as<uint32_t>();
+    ap.off = g == 1 ? nullptr : w.ol[g & 1].as<uint32_t>();
+    ap.knext = w.knext.as<uint32_t>();
     ap.kuni = K1, ap.sub_n = 1, ap.sub_j = 0;
     ap.min_spp = prm->min_spp, ap.budget = budget, ap.phase = g, ap.kcap = kcap;
     // a phase of at least ~phase_slots slots while pixels remain: once few pixels are left,
@@ -785,16 +792,19 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ap.rec_segs = A.counters + 9;
     ap.next_active = ctr + kSpreadBase;
     // (ap.next_active was zeroed with the phase's slot counter block, k_slot_block_init)
-    hipLaunchKernelGGL(k_adapt_record, dim3((unsigned)((npix + 63) / 64)), dim3(64), 0, s, px, Lph, npix, npix, ap);
+    const int64_t n = active;  // entries of the phase's list
+    hipLaunchKernelGGL(k_adapt_record, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, px, Lph, n, npix, ap);
     HIPC(hipGetLastError());
-    hipLaunchKernelGGL(k_adapt_floor, dim3(qb), dim3(kBlock), 0, s, ap.knext, npix, 1, 0, (const int32_t*)px.samples,
-                       budget, kcap, phase_slots, (const unsigned long long*)ap.next_active, ctr + 8 * 16 + 1);
+    hipLaunchKernelGGL(k_adapt_floor, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ap.knext, ap.list,
+                       n, 1, 0, (const int32_t*)px.samples, budget, kcap, phase_slots,
+                       (const unsigned long long*)ap.next_active, ctr + 8 * 16 + 1);
     HIPC(hipGetLastError());
-    HIPC(rtxscan::exclusive_scan_u32(ap.knext, w.off.as<uint32_t>(), npix, w.scan_tmp.p, w.scan_tmp.n, s));
-    hipLaunchKernelGGL(k_adapt_expand, dim3((unsigned)((npix + kExpandPix - 1) / kExpandPix)), dim3(kBlock), 0, s,
-                       (const uint32_t*)ap.knext,
-                       (const uint32_t*)w.off.as<uint32_t>(), npix, 1, 0, (const int32_t*)px.samples,
-                       w.smap.as<uint2>(), ctr + 8 * 16);
+    HIPC(rtxscan::exclusive_scan_packed(ap.knext, w.pk.as<uint64_t>(), n, w.scan_tmp.p, w.scan_tmp.n, s));
+    const AdaptList next{w.lst[(g + 1) & 1].as<uint32_t>(), w.kl[(g + 1) & 1].as<uint32_t>(),
+                         w.ol[(g + 1) & 1].as<uint32_t>()};
+    hipLaunchKernelGGL(k_adapt_expand, dim3((unsigned)((n + kExpandPix - 1) / kExpandPix)), dim3(kBlock), 0, s,
+                       (const uint32_t*)ap.knext, (const unsigned long long*)w.pk.as<unsigned long long>(), ap.list, n,
+                       1, 0, (const int32_t*)px.samples, w.smap.as<uint2>(), next, ctr + 8 * 16);
     HIPC(hipGetLastError());
     HIPC(hipMemcpyAsync(w.total_h.p, ctr + 8 * 16, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     HIPC(hipEventRecord(w.ev, s));

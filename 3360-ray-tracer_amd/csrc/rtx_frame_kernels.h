@@ -97,41 +97,52 @@ struct PixRec {
   int n;
   bool conv;
 };
-__device__ __forceinline__ void record_sample(PixRec& r, const double (&x)[3], int min_spp, double rel) {
+// delta / n exactly as the IEEE division rounds it, from y = RN(1 / n) and one correction
+// (Markstein: q = RN(delta y) is within an ulp of delta / n, r = delta - q n is exact by fma,
+// RN(q + r y) is the correctly rounded quotient; checked bit for bit against the division on
+// 2e8 quotients, near-ties included, tests/test_record_division.py).  Zero, tiny (where the
+// theorem's no-underflow condition could fail) and non-finite deltas take the division.
+__device__ __forceinline__ double div_by_count(double delta, double n, double y) {
+  double q = delta * y;
+  q = fma(fma(-q, n, delta), y, q);
+  if (__builtin_expect(!(fabs(delta) >= 0x1p-900 && fabs(delta) < INFINITY), 0)) q = delta / n;
+  return q;
+}
+// RecordSample's update (pixel_state.h:22-39) of one radiance record x
+__device__ __forceinline__ void record_update(PixRec& r, const double (&x)[3]) {
   r.n++;
+  const double dn = (double)r.n, y = 1.0 / dn;  // (one division per sample, for the three channels)
   for (int c = 0; c < 3; c++) {
     double mu = r.mean[c];
     double delta = x[c] - mu;
-    mu += delta / r.n;
+    mu += div_by_count(delta, dn, y);
     double delta2 = x[c] - mu;
     r.mean[c] = mu;
     r.m2[c] += delta2 * delta;
   }
   for (int c = 0; c < 3; c++) r.sum[c] += x[c];
-  if (r.n >= min_spp) {
-    // err / mu > rel  <=>  m2 > rel^2 (n - 1) n mu^2 up to the few ulps the exact form rounds
-    // by: decided by products where the two sides differ by more than 1e-10 relative (the
-    // usual case), the exact form (two divisions, two square roots) only in between; NaN
-    // fails both comparisons and takes the exact form too.
-    // (channels in order, the first failing one decides; unrolled, so the statistics stay in
-    // registers)
-    bool ok = true;
+}
+// IsConverged (pixel_state.h:54-72) of the statistics after the update, once n >= min_spp:
+// err / mu > rel  <=>  m2 > rel^2 (n - 1) n mu^2 up to the few ulps the exact form rounds by,
+// so the products decide where the two sides differ by more than 1e-10 relative (the usual
+// case), the exact form (two divisions, two square roots) only in between; NaN fails both
+// comparisons and takes the exact form too.  (All channels must pass: a conjunction, so the
+// order of the reference's early exit does not matter.)
+__device__ __forceinline__ bool record_converged(const PixRec& r, int min_spp, double rel) {
+  if (r.n < min_spp) return false;
+  bool ok = true;
 #pragma unroll
-    for (int c = 0; c < 3; c++) {
-      if (ok) {
-        double mu = fmax(fabs(r.mean[c]), 1e-3);
-        const double thr = rel * rel * ((double)(r.n - 1) * (double)r.n * (mu * mu));
-        if (r.m2[c] > thr * (1.0 + 1e-10)) {
-          ok = false;
-        } else if (!(r.m2[c] < thr * (1.0 - 1e-10))) {
-          double var = r.n > 1 ? r.m2[c] / (r.n - 1) : 0.0;
-          double err = sqrt(var) / sqrt((double)r.n);
-          if (err / mu > rel) ok = false;
-        }
-      }
+  for (int c = 0; c < 3; c++) {
+    const double mu = fmax(fabs(r.mean[c]), 1e-3);
+    const double thr = rel * rel * ((double)(r.n - 1) * (double)r.n * (mu * mu));
+    if (r.m2[c] > thr * (1.0 + 1e-10)) ok = false;
+    else if (__builtin_expect(!(r.m2[c] < thr * (1.0 - 1e-10)), 0)) {
+      double var = r.n > 1 ? r.m2[c] / (r.n - 1) : 0.0;
+      double err = sqrt(var) / sqrt((double)r.n);
+      if (err / mu > rel) ok = false;
     }
-    r.conv = ok;
   }
+  return ok;
 }
 __device__ __forceinline__ void load_pixel(PixRec& r, const PixelSoA& px, int64_t npix, int64_t p) {
   for (int c = 0; c < 3; c++) r.sum[c] = px.sum[c * npix + p], r.mean[c] = px.mean[c * npix + p], r.m2[c] = px.m2[c * npix + p];
@@ -204,9 +215,13 @@ __global__ __launch_bounds__(kBlock) void k_accumulate(PixelSoA px, const double
 // sizes are: the prediction only decides how much work is spent and how many phases it takes.
 // ---------------------------------------------------------------------------------------
 struct AdaptPlan {
-  const uint32_t* kcur;  // samples of sub-pixel q in the phase just traced (nullptr: kuni each)
-  const uint32_t* off;   // their first slot (nullptr: the uniform first phase, p * kuni)
-  uint32_t* knext;       // out: samples of q in the next phase (0: q is finished)
+  // entry i of the phase just traced: sub-pixel list[i] (nullptr: the uniform first phase, every
+  // sub-pixel, q = i), its samples kcur[i] (nullptr: kuni each), their first slot off[i]
+  // (nullptr: p * kuni)
+  const uint32_t* list;
+  const uint32_t* kcur;
+  const uint32_t* off;
+  uint32_t* knext;       // out: samples of entry i in the next phase (0: finished)
   int32_t kuni;
   int32_t sub_n, sub_j;  // pixel p = q * sub_n + sub_j
   int32_t min_spp, budget, phase, kcap;
@@ -244,31 +259,30 @@ constexpr int kSpread = 64, kSpreadStride = 16;
 // consecutive 8-byte pieces of one run, so an instruction touches 8 runs (~12 cache lines)
 // instead of 64; each lane then replays its own run from LDS.  The next window's loads are in
 // flight while the current one is replayed.
-#ifndef RTX_REC_WIN
-#define RTX_REC_WIN 8
-#endif
-constexpr int kRecWin = RTX_REC_WIN, kRecPieces = 3 * kRecWin,
-              kRecPitch = kRecPieces + 1,  // (odd pitch: a lane's row starts on another bank)
-    kRecLpr = 8,                           // lanes per run in a load instruction
-    kRecRuns = 64 / kRecLpr,               // runs per load instruction
-    kRecGroups = (kRecPieces + kRecLpr - 1) / kRecLpr;  // load instructions per run and window
-__global__ __launch_bounds__(64) void k_adapt_record(PixelSoA px, const double* __restrict__ L, int64_t nq,
+// (8-sample windows: 16-sample windows, 186 VGPRs, measured slower after the first phase: r8e)
+constexpr int kRecLpr = 8,      // lanes per run in a load instruction
+    kRecRuns = 64 / kRecLpr;    // runs per load instruction
+__global__ __launch_bounds__(64) void k_adapt_record(PixelSoA px, const double* __restrict__ L, int64_t n,
                                                      int64_t npix, AdaptPlan ap) {
+  constexpr int kRecWin = 8, kRecPieces = 3 * kRecWin,
+                kRecPitch = kRecPieces + 1,  // (odd pitch: a lane's row starts on another bank)
+      kRecGroups = (kRecPieces + kRecLpr - 1) / kRecLpr;  // load instructions per run and window
   __shared__ double s_win[64 * kRecPitch];
   __shared__ int64_t s_base[64];  // the lane's first radiance word
   __shared__ int32_t s_n[64];     // its words in the window being fetched
   const int lane = (int)threadIdx.x;
-  const int64_t q = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;  // entry of the phase's pixel list
   int64_t p = 0, base = 0;
   int K = 0;
   bool act = false;
   PixRec r;
   r.n = 0, r.conv = false;
-  if (q < nq) {
+  if (i < n) {
+    const int64_t q = ap.list ? (int64_t)ap.list[i] : i;
     p = q * ap.sub_n + ap.sub_j;
-    K = ap.kcur ? (int)ap.kcur[q] : ap.kuni;
+    K = ap.kcur ? (int)ap.kcur[i] : ap.kuni;
     act = K > 0 && !px.conv[p];
-    base = 3 * (ap.off ? (int64_t)ap.off[q] : p * (int64_t)ap.kuni);
+    base = 3 * (ap.off ? (int64_t)ap.off[i] : p * (int64_t)ap.kuni);
     if (act) load_pixel(r, px, npix, p);
   }
   const int n0 = r.n;
@@ -281,8 +295,8 @@ __global__ __launch_bounds__(64) void k_adapt_record(PixelSoA px, const double* 
 #pragma unroll
   for (int j = 0; j < kRecRuns; j++) rp[j] = L + s_base[kRecRuns * j + a] + b;
   double v[kRecRuns * kRecGroups];
-  uint32_t got = 0;
-  static_assert(kRecRuns * kRecGroups <= 32, "got: one bit per load");
+  uint64_t got = 0;
+  static_assert(kRecRuns * kRecGroups <= 64, "got: one bit per load");
   auto fetch = [&](int t) {  // the window of samples [t, t + kRecWin) of every lane's run
     got = 0;
 #pragma unroll
@@ -290,7 +304,8 @@ __global__ __launch_bounds__(64) void k_adapt_record(PixelSoA px, const double* 
       const int nj = s_n[kRecRuns * j + a];
 #pragma unroll
       for (int g = 0; g < kRecGroups; g++)
-        if (kRecLpr * g + b < nj) v[j * kRecGroups + g] = rp[j][3 * t + kRecLpr * g], got |= 1u << (j * kRecGroups + g);
+        if (kRecLpr * g + b < nj)
+          v[j * kRecGroups + g] = rp[j][3 * t + kRecLpr * g], got |= 1ull << (j * kRecGroups + g);
     }
   };
   fetch(0);
@@ -308,11 +323,14 @@ __global__ __launch_bounds__(64) void k_adapt_record(PixelSoA px, const double* 
     const bool more = __ballot(nn > 0) != 0ull;
     if (more) fetch(t + kRecWin);
     if (act && !r.conv) {
+      // (a straight-line pass over the window, IsConverged noted rather than branched on and the
+      // converging window replayed again, measured slower: 527 vs 460 us per frame, r8e / r8f)
       const double* w = s_win + lane * kRecPitch;
       const int c = min(K - t, kRecWin);
       for (int k = 0; k < c && !r.conv; k++) {
         const double x[3] = {w[3 * k], w[3 * k + 1], w[3 * k + 2]};
-        record_sample(r, x, ap.min_spp, ap.rel);
+        record_update(r, x);
+        r.conv = record_converged(r, ap.min_spp, ap.rel);
       }
     }
     if (!more) break;
@@ -328,7 +346,7 @@ __global__ __launch_bounds__(64) void k_adapt_record(PixelSoA px, const double* 
     store_pixel(r, px, npix, p);
     if (!r.conv && r.n < ap.budget) kn = adapt_next_batch(r.mean, r.m2, r.n, ap);
   }
-  if (q < nq) ap.knext[q] = kn;
+  if (i < n) ap.knext[i] = kn;
   const unsigned long long na = __popcll(__ballot(kn != 0));
   if (na && lane == 0) atomicAdd(ap.next_active + (blockIdx.x % kSpread) * kSpreadStride, na);
 }
@@ -337,61 +355,73 @@ __global__ __launch_bounds__(64) void k_adapt_record(PixelSoA px, const double* 
 // fill the GPU, and the pixels finish in it rather than in further phases that would be mostly
 // launch drain (the last paths of a launch run with their waves nearly empty).
 // It also writes that count (the next phase's pixels) for the host (*pixels).
-__global__ __launch_bounds__(kBlock) void k_adapt_floor(uint32_t* __restrict__ knext, int64_t nq, int32_t sub_n,
+__global__ __launch_bounds__(kBlock) void k_adapt_floor(uint32_t* __restrict__ knext, const uint32_t* __restrict__ list,
+                                                        int64_t n, int32_t sub_n,
                                                         int32_t sub_j, const int32_t* __restrict__ samples,
                                                         int32_t budget, int32_t kcap, int64_t target,
                                                         const unsigned long long* __restrict__ next_active,
                                                         unsigned long long* __restrict__ pixels) {
-  const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   static_assert(kSpread == 64, "one spread counter per lane");
   unsigned long long na = next_active[lane_id() * kSpreadStride];
   for (int m = 32; m >= 1; m >>= 1) na += (unsigned long long)__shfl_xor((long long)na, m);
-  if (q == 0) *pixels = na;
-  if (q >= nq) return;
-  const uint32_t k = knext[q];
+  if (i == 0) *pixels = na;
+  if (i >= n) return;
+  const uint32_t k = knext[i];
   if (k == 0) return;
+  const int64_t q = list ? (int64_t)list[i] : i;
   const int64_t kmin = (target + (int64_t)na - 1) / (int64_t)max(na, 1ull);
   const int left = budget - samples[q * sub_n + sub_j];
   int kn = (int)max<int64_t>((int64_t)k, min<int64_t>(kmin, (int64_t)left));
   kn = (kn + 3) & ~3;
-  knext[q] = (uint32_t)min(kn, min(left, kcap));
+  knext[i] = (uint32_t)min(kn, min(left, kcap));
 }
-// The next phase's slot map: sub-pixel q's batch occupies slots [off[q], off[q] + knext[q]),
-// slot off[q] + k being sample samples[p] + k of pixel p.  One block per kExpandPix sub-pixels;
-// its slots are a contiguous range written by all its threads (coalesced), each finding its
-// sub-pixel by a search of the block's offsets in LDS.  The last sub-pixel's thread writes the
-// phase's slot count and the map's address (k_adapt_floor wrote its pixel count).  (Few pixels per block: the pixels still sampling cluster, and a block
-// over 256 of them had up to 256 x kcap slots to write while most blocks had none.)
+// The next phase's slot map and pixel list.  Entry i of the phase just recorded (sub-pixel
+// list[i]) has knext[i] samples in the next phase; pk[i] (exclusive_scan_packed) holds their
+// first slot (high word) and, when knext[i] != 0, the entry's index in the next list (low
+// word).  The batch occupies slots [hi, hi + knext[i]), slot hi + k being sample samples[p] + k
+// of pixel p, and the next list's entry gets (sub-pixel, samples, first slot).  One block per
+// kExpandPix entries; its slots are a contiguous range written by all its threads (coalesced),
+// each finding its entry by a search of the block's offsets in LDS.  The last entry's thread
+// writes the phase's slot count and the map's address (k_adapt_floor wrote its pixel count).
+// (Few entries per block: a block over 256 of them had up to 256 x kcap slots to write.)
 constexpr int kExpandPix = 32;
+struct AdaptList {  // a phase's pixel list: entry i = sub-pixel q[i], k[i] samples from slot off[i]
+  uint32_t *q, *k, *off;
+};
 __global__ __launch_bounds__(kBlock) void k_adapt_expand(const uint32_t* __restrict__ knext,
-                                                         const uint32_t* __restrict__ off, int64_t nq, int32_t sub_n,
+                                                         const unsigned long long* __restrict__ pk,
+                                                         const uint32_t* __restrict__ list, int64_t n, int32_t sub_n,
                                                          int32_t sub_j, const int32_t* __restrict__ samples,
-                                                         uint2* __restrict__ smap,
+                                                         uint2* __restrict__ smap, AdaptList next,
                                                          unsigned long long* __restrict__ total) {
   __shared__ uint32_t s_off[kExpandPix], s_p[kExpandPix], s_s0[kExpandPix];
   __shared__ uint32_t s_end;
   const int t = threadIdx.x;
-  const int64_t q0 = (int64_t)blockIdx.x * kExpandPix, q = q0 + t;
-  const int nb = (int)min<int64_t>(kExpandPix, nq - q0);
+  const int64_t i0 = (int64_t)blockIdx.x * kExpandPix, i = i0 + t;
+  const int nb = (int)min<int64_t>(kExpandPix, n - i0);
   if (t < nb) {
-    const uint32_t k = knext[q], o = off[q];
-    const int64_t p = q * sub_n + sub_j;
+    const uint32_t k = knext[i];
+    const unsigned long long v = pk[i];
+    const uint32_t o = (uint32_t)(v >> 32), idx = (uint32_t)v;
+    const int64_t q = list ? (int64_t)list[i] : i, p = q * sub_n + sub_j;
     s_off[t] = o, s_p[t] = (uint32_t)p, s_s0[t] = k ? (uint32_t)samples[p] : 0u;
+    if (k) next.q[idx] = (uint32_t)q, next.k[idx] = k, next.off[idx] = o;
     if (t == nb - 1) {
       s_end = o + k;
-      if (q == nq - 1) total[0] = (unsigned long long)o + k, total[2] = (unsigned long long)smap;
+      if (i == n - 1) total[0] = (unsigned long long)o + k, total[2] = (unsigned long long)smap;
     }
   }
   __syncthreads();
   const uint32_t b = s_off[0], e = s_end;
-  for (uint32_t i = b + t; i < e; i += kBlock) {
-    int lo = 0, hi = nb;  // the last q with s_off[q] <= i (a zero batch shares its successor's offset)
+  for (uint32_t j = b + t; j < e; j += kBlock) {
+    int lo = 0, hi = nb;  // the last entry with s_off <= j (a zero batch shares its successor's offset)
     while (hi - lo > 1) {
       const int mid = (lo + hi) >> 1;
-      if (s_off[mid] <= i) lo = mid;
+      if (s_off[mid] <= j) lo = mid;
       else hi = mid;
     }
-    smap[i] = make_uint2(s_p[lo], s_s0[lo] + (i - s_off[lo]));
+    smap[j] = make_uint2(s_p[lo], s_s0[lo] + (j - s_off[lo]));
   }
 }
 

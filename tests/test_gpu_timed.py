@@ -183,7 +183,8 @@ def test_adaptive_recorded_segments_equal_oracle(rtx_mod, orc, scenes, acase, ro
 # with the oracle on sample counts, recorded segments and pixels.
 FULL_BUDGET_CASES = [(1, 200, 0.7), (3, 2048, 0.5)]  # bench case index, spp, band row (fraction of H)
 TUNES = {"phases": {}, "phases_small": dict(phase_slots=4096, phase_kcap=8),
-         "phases_kcap4": dict(phase_slots=64, phase_kcap=4), "phases_first_uniform": dict(first_map=0)}
+         "phases_kcap4": dict(phase_slots=64, phase_kcap=4), "phases_first_uniform": dict(first_map=0),
+         "phases_floor_2e23": dict(phase_slots=1 << 23)}
 
 
 @pytest.mark.parametrize("tune", sorted(TUNES))
