@@ -130,9 +130,9 @@ struct BandSink {
 constexpr int kBands = 8;  // bands of the last accumulate and of the D2H copies that overlap them (ab_bands_*: 2 / 4 / 8 / 16)
 
 // Adaptive renders in phases (render_adaptive)
-// render_adaptive: the smallest phase planned while pixels remain (r05 r8d / r8e: 2^20 +0.8-1.0 %
-// against round 3's 2^23 on C3 adaptive; scripts/adaptive_sim.py ranks the floors offline)
-constexpr int64_t kAdaptPhaseSlots = 1 << 20;
+// render_adaptive: the smallest phase planned while pixels remain (round 3: 2^23; with the pooled
+// prediction 2^21, scripts/adaptive_sim.py and r05 r8j / r8k)
+constexpr int64_t kAdaptPhaseSlots = 1 << 21;
 constexpr double kAdaptMarginStep = 0.25;      // render_adaptive: batch margin 1 + step * (phase - 1) (0.5: within noise, r3y)
 // Overrides of the adaptive schedules' constants (0: the default): rtx_internal_adapt_tune, a
 // test and tuning hook (not in rtx.h) that forces small workspaces and floors, so the paths
@@ -142,8 +142,15 @@ struct AdaptTune {
   int phase_kcap;       // phases: the largest batch of one pixel (else from the workspace)
   int first_map;         // the uniform first pass: 1 the phase kernel (block-shared chunks), 0 the uniform-group one (< 0: default)
   double phase_mstep;    // phases: the batch margin's growth per phase (< 0: kAdaptMarginStep)
+  double margin1;        // the margin of the batches after the first phase (< 0: kAdaptMargin1)
+  double pool_w;         // the pooled prediction's centre weight (< 0: kAdaptPoolW; 0: not pooled)
 };
-static AdaptTune g_tune{0, 0, -1, -1.0};
+static AdaptTune g_tune{0, 0, -1, -1.0, -1.0, -1.0};
+// render_adaptive: the margin of the batches after the first phase, and k_adapt_plan's centre
+// weight (0: each pixel's own prediction only): ranked first by scripts/adaptive_sim.py, then
+// C3 adaptive +4.0 %, C2 +0.5 % against the unpooled margin 1.0 (r05 r8j / r8k)
+constexpr double kAdaptMargin1 = 0.8;
+constexpr double kAdaptPoolW = 8.0;
 constexpr int kFirstPassMap = 1;  // the adaptive first pass runs the phase kernel (MAP 1, no slot map)
 // RTX_DEBUG_HOST: host-side timestamps of a frame (render_stripes_to_host prints them, with the
 // device; per thread: rtx_render_multi renders each device on a thread of its own)
@@ -155,12 +162,13 @@ static thread_local double g_t_launch = 0, g_t_sync0 = 0, g_t_sync1 = 0;
 struct AdaptWs {
   // lst / kl / ol: the phases' pixel lists (ping-pong: sub-pixel, samples, first slot per entry);
   // knext: the next batch per entry of the phase just traced; pk: their packed prefix sums
-  DevBuf lbuf, smap, lst[2], kl[2], ol[2], knext, pk, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer, then the spread pixel counts (kSpreadBase)
+  // rv: each pixel's predicted convergence count at its last record (k_adapt_plan's pooling)
+  DevBuf lbuf, smap, lst[2], kl[2], ol[2], knext, pk, rv, scan_tmp, ctr;  // ctr: 8 region slot counters (128 B apart), then u64 slot count, pixel count, slot map address, ..., [132] segment buffer, then the spread pixel counts (kSpreadBase)
   DevBuf segs;                                  // counting renders: each slot's path segments (u16)
   HostBuf total_h;                              // pinned copy of the next phase's slot count
   hipEvent_t ev = nullptr;                      // total_h written
   void release() {
-    for (DevBuf* b : {&lbuf, &smap, &lst[0], &lst[1], &kl[0], &kl[1], &ol[0], &ol[1], &knext, &pk, &scan_tmp, &ctr,
+    for (DevBuf* b : {&lbuf, &smap, &lst[0], &lst[1], &kl[0], &kl[1], &ol[0], &ol[1], &knext, &pk, &rv, &scan_tmp, &ctr,
                       &segs})
       b->release();
     total_h.release();
@@ -766,6 +774,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     for (DevBuf* b : {&w.lst[0], &w.lst[1], &w.kl[0], &w.kl[1], &w.ol[0], &w.ol[1], &w.knext})
       if ((rc = b->reserve(npix * sizeof(uint32_t)))) return rc;
     if ((rc = w.pk.reserve(npix * sizeof(unsigned long long)))) return rc;
+    if ((rc = w.rv.reserve(npix * sizeof(float)))) return rc;
     if ((rc = w.scan_tmp.reserve(std::max<size_t>(16, rtxscan::temp_bytes_packed(npix))))) return rc;
     if ((rc = w.ctr.reserve(kAdaptCtrWords * sizeof(unsigned long long)))) return rc;
     if ((rc = w.total_h.reserve(2 * sizeof(unsigned long long)))) return rc;
@@ -788,6 +797,10 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     ap.kmin = (int32_t)std::min<int64_t>(budget, (phase_slots + active - 1) / std::max<int64_t>(1, active));
     ap.rel = prm->rel_threshold;
     ap.margin_step = g_tune.phase_mstep >= 0 ? g_tune.phase_mstep : kAdaptMarginStep;
+    ap.margin1 = g_tune.margin1 >= 0 ? g_tune.margin1 : kAdaptMargin1;
+    ap.pool_w = (float)(g_tune.pool_w >= 0 ? g_tune.pool_w : kAdaptPoolW);
+    ap.rv = w.rv.as<float>();
+    ap.width = std::max(1, A.map.stripes ? A.map.W : A.map.w);  // (the render's own rows)
     ap.segs = !L.count ? nullptr : g == 1 ? sc->segs1.as<uint16_t>() : w.segs.as<uint16_t>();
     ap.rec_segs = A.counters + 9;
     ap.next_active = ctr + kSpreadBase;
@@ -795,6 +808,10 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     const int64_t n = active;  // entries of the phase's list
     hipLaunchKernelGGL(k_adapt_record, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, px, Lph, n, npix, ap);
     HIPC(hipGetLastError());
+    if (ap.pool_w > 0.0f) {
+      hipLaunchKernelGGL(k_adapt_plan, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, px, n, npix, ap);
+      HIPC(hipGetLastError());
+    }
     hipLaunchKernelGGL(k_adapt_floor, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ap.knext, ap.list,
                        n, 1, 0, (const int32_t*)px.samples, budget, kcap, phase_slots,
                        (const unsigned long long*)ap.next_active, ctr + 8 * 16 + 1);
@@ -1847,9 +1864,10 @@ extern "C" int rtx_internal_check_sincos(int device, int64_t n, uint64_t seed, i
 // one) and the batch margin's growth per phase.  Results never depend on them, only the amount
 // of work and the number of phases do (tests/test_gpu_timed.py runs the full budgets through
 // forced small workspaces).
-extern "C" int rtx_internal_adapt_tune(int64_t phase_slots, int32_t phase_kcap, int32_t first_map, double phase_mstep) {
+extern "C" int rtx_internal_adapt_tune(int64_t phase_slots, int32_t phase_kcap, int32_t first_map, double phase_mstep,
+                                       double margin1, double pool_w) {
   if (phase_slots < 0 || phase_kcap < 0 || first_map > 1) return fail(RTX_ERR_INVALID, "bad tuning value");
-  g_tune = AdaptTune{phase_slots, phase_kcap, first_map, phase_mstep};
+  g_tune = AdaptTune{phase_slots, phase_kcap, first_map, phase_mstep, margin1, pool_w};
   return RTX_OK;
 }
 

@@ -228,21 +228,31 @@ struct AdaptPlan {
   int32_t kmin;  // smallest next batch: keeps a phase with few pixels left large enough to fill the GPU
   double rel;
   double margin_step;  // the batch margin grows by this much per phase (1 + step * (phase - 1))
+  double margin1;      // ... except after the first phase: this margin
+  // the prediction pooled over the pixel's 3 x 3 neighbourhood (k_adapt_plan) when pool_w > 0:
+  // need(p) weighted pool_w, each neighbour's 1; rv holds every pixel's need at its last record,
+  // in the render's own pixel grid of `width` columns
+  float* rv;
+  float pool_w;
+  int32_t width;
   const uint16_t* segs;           // counting renders: segments of each slot's path (else nullptr)
   unsigned long long* rec_segs;   // ... summed here over the samples the pixels record
   unsigned long long* next_active;  // the next phase's pixel count, in kSpread words kSpreadStride
                                     // apart (added here, zeroed before the launch; k_adapt_floor sums)
 };
-__device__ __forceinline__ uint32_t adapt_next_batch(const double (&mean)[3], const double (&m2)[3], int n,
-                                                     const AdaptPlan& ap) {
-  double need = 0.0;  // samples at which IsConverged would hold with the current estimates
+// samples at which IsConverged would hold with the current estimates
+__device__ __forceinline__ double adapt_need(const double (&mean)[3], const double (&m2)[3], int n, double rel) {
+  double need = 0.0;
   for (int c = 0; c < 3; c++) {
     const double var = n > 1 ? m2[c] / (n - 1) : 0.0;
     const double mu = fmax(fabs(mean[c]), 1e-3);
-    need = fmax(need, var / (ap.rel * ap.rel * mu * mu));
+    need = fmax(need, var / (rel * rel * mu * mu));
   }
+  return need;
+}
+__device__ __forceinline__ uint32_t adapt_next_batch(double need, int n, const AdaptPlan& ap) {
   const int left = ap.budget - n;
-  const double margin = 1.0 + ap.margin_step * (double)(ap.phase - 1);
+  const double margin = ap.phase == 1 ? ap.margin1 : 1.0 + ap.margin_step * (double)(ap.phase - 1);
   const double want = (need - (double)n) * margin;
   int k = (want < (double)left) ? (int)ceil(want) : left;  // NaN / inf: the whole budget
   k = max(k, min(max(4 << min(ap.phase - 1, 4), ap.kmin), left));  // at least 4, 8, ... 64 more, and kmin
@@ -252,6 +262,11 @@ __device__ __forceinline__ uint32_t adapt_next_batch(const double (&mean)[3], co
 // Counters that every wave of a launch adds to are spread over kSpread words kSpreadStride words
 // apart (a device-scope atomic add to one word serialises at ~10 ns per wave)
 constexpr int kSpread = 64, kSpreadStride = 16;
+// A wave's continuing pixels, added to the spread word of its block (every lane takes part).
+__device__ __forceinline__ void spread_add(unsigned long long* base, uint32_t kn) {
+  const unsigned long long na = __popcll(__ballot(kn != 0));
+  if (na && lane_id() == 0) atomicAdd(base + (blockIdx.x % kSpread) * kSpreadStride, na);
+}
 // One lane per sub-pixel, one wave per block: the replay of a pixel's samples is sequential
 // (each step divides by the running count), so the parallelism is across pixels.  The wave's
 // 64 runs of the phase's radiance records (each contiguous: pixel-major slots) come in windows
@@ -344,17 +359,47 @@ __global__ __launch_bounds__(64) void k_adapt_record(PixelSoA px, const double* 
       atomicAdd(ap.rec_segs, t);
     }
     store_pixel(r, px, npix, p);
-    if (!r.conv && r.n < ap.budget) kn = adapt_next_batch(r.mean, r.m2, r.n, ap);
+    const double need = adapt_need(r.mean, r.m2, r.n, ap.rel);
+    if (ap.pool_w > 0.0f) ap.rv[p] = (float)need;  // k_adapt_plan sizes the batch
+    else if (!r.conv && r.n < ap.budget) kn = adapt_next_batch(need, r.n, ap);
   }
+  if (ap.pool_w > 0.0f) return;
   if (i < n) ap.knext[i] = kn;
-  const unsigned long long na = __popcll(__ballot(kn != 0));
-  if (na && lane == 0) atomicAdd(ap.next_active + (blockIdx.x % kSpread) * kSpreadStride, na);
+  spread_add(ap.next_active, kn);
+}
+// The next batches from the prediction pooled over each pixel's 3 x 3 neighbourhood (after
+// k_adapt_record, when ap.pool_w > 0): a pixel's relative variance is a property of what it
+// sees, shared with its neighbours, and 16 samples estimate it poorly; the pooled estimate sizes
+// the batch (the result does not depend on it, only the work and the phases do).
+__global__ __launch_bounds__(kBlock) void k_adapt_plan(PixelSoA px, int64_t n, int64_t npix, AdaptPlan ap) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  uint32_t kn = 0;
+  if (i < n) {
+    const int64_t q = ap.list ? (int64_t)ap.list[i] : i, p = q * ap.sub_n + ap.sub_j;
+    const int ns = px.samples[p];
+    if (!px.conv[p] && ns < ap.budget) {
+      const int64_t w = ap.width, x = p % w, y = p / w;
+      float acc = ap.pool_w * ap.rv[p], wsum = ap.pool_w;
+      for (int dy = -1; dy <= 1; dy++)
+        for (int dx = -1; dx <= 1; dx++) {
+          const int64_t xx = x + dx, yy = y + dy, pp = yy * w + xx;
+          if ((dx | dy) == 0 || xx < 0 || xx >= w || yy < 0 || pp >= npix) continue;
+          const float v = ap.rv[pp];
+          if (v == v) acc += v, wsum += 1.0f;
+        }
+      kn = adapt_next_batch((double)(acc / wsum), ns, ap);
+    }
+    ap.knext[i] = kn;
+  }
+  spread_add(ap.next_active, kn);
 }
 // Once the next phase's pixel count is known: every batch at least target / that count (within
 // the pixel's budget and the workspace), so a phase with few pixels left is large enough to
 // fill the GPU, and the pixels finish in it rather than in further phases that would be mostly
-// launch drain (the last paths of a launch run with their waves nearly empty).
-// It also writes that count (the next phase's pixels) for the host (*pixels).
+// launch drain (the last paths of a launch run with their waves nearly empty).  (Finishing every
+// pixel in the next phase whenever that adds fewer than 2^22 slots measured +0.3 % on C3,
+// -0.2 % on C2: not kept, profiles/r05/ab/ab_adaptive_policy_r8k.txt.)
+// It also writes the next phase's pixel count for the host (*pixels).
 __global__ __launch_bounds__(kBlock) void k_adapt_floor(uint32_t* __restrict__ knext, const uint32_t* __restrict__ list,
                                                         int64_t n, int32_t sub_n,
                                                         int32_t sub_j, const int32_t* __restrict__ samples,

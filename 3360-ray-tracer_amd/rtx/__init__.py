@@ -352,17 +352,19 @@ class DeviceScene:
         return st.as_dict() if stats else None
 
 
-def adapt_tune(phase_slots=0, phase_kcap=0, first_map=-1, phase_mstep=-1.0):
+def adapt_tune(phase_slots=0, phase_kcap=0, first_map=-1, phase_mstep=-1.0, margin1=-1.0, pool_w=-1.0):
     """Test / tuning hook (rtx_internal_adapt_tune, not in rtx.h): overrides of the adaptive
     phases' constants for the renders that follow in this process; no argument restores the
     defaults.  Results never depend on them, only the work and the phases do.  phase_slots: the
     smallest phase while pixels remain; phase_kcap: the largest batch of one pixel; first_map:
     the uniform first pass on the phase kernel (1, block-shared chunks) or on the uniform-group
-    kernel (0); phase_mstep: the batch margin's growth per phase."""
+    kernel (0); phase_mstep: the batch margin's growth per phase; margin1: the margin of the
+    batches after the first phase; pool_w: the centre weight of the prediction pooled over each
+    pixel's 3 x 3 neighbourhood (k_adapt_plan; 0: each pixel's own prediction)."""
     f = lib().rtx_internal_adapt_tune
-    f.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_double]
+    f.argtypes = [C.c_int64, C.c_int32, C.c_int32, C.c_double, C.c_double, C.c_double]
     f.restype = C.c_int
-    _check(f(phase_slots, phase_kcap, first_map, phase_mstep), "rtx_internal_adapt_tune")
+    _check(f(phase_slots, phase_kcap, first_map, phase_mstep, margin1, pool_w), "rtx_internal_adapt_tune")
 
 
 def render_multi(scenes, cam, spp, max_depth, seed=1234, adaptive=True, mode="persistent", precision="fast",

@@ -172,7 +172,7 @@ def main():
 
     if args.adapt_tune:
         kv = dict(x.split("=") for x in args.adapt_tune.split(","))
-        rtx.adapt_tune(**{k: (float(v) if k in ("phase_mstep",) else int(v)) for k, v in kv.items()})
+        rtx.adapt_tune(**{k: (float(v) if k in ("phase_mstep", "margin1", "pool_w") else int(v)) for k, v in kv.items()})
     workload = args.workload if args.workload != "auto" else ("c3_bunny" if world == 1 else "c4_bunny4k")
     scene_name, preset, width, spp, depth = WORKLOADS[workload]
     spp = args.spp or spp

@@ -9,11 +9,10 @@ discarded), only the work does: per phase, the slots, traced segments and pixels
 cost model (segments / rate + a drain per launch + per-phase fixed costs) this ranks policy
 variants before they are measured on the GPU.
 
-  python3 scripts/adaptive_sim.py [--workload c3_bunny] [--cache /tmp/c3_samples.npz] \
-      [--variants default,floor22,...]
+  python3 scripts/adaptive_sim.py [--workload c3_bunny|c2_final] [--cache /tmp/adaptive_sim_c3.npz]
+(profiles/r05/adaptive_sim_policies.txt: the policy grids this round's defaults came from)
 """
 import argparse
-import math
 import os
 import sys
 import time
@@ -76,7 +75,8 @@ def prepare(L, segs):
 
 
 def simulate(pre, budget, phase_slots=1 << 23, mstep=0.25, kmin_first=True, floor=True, min_batch=(4, 4),
-             first=MIN_SPP, kcap=None, margins=None, floor_from=2):
+             first=MIN_SPP, kcap=None, margins=None, floor_from=2, pool=0, width=None, pool_w=1.0,
+             finish_slots=None):
     """Replays the phase policy; returns per-phase dicts (pixels, slots, traced and recorded
     segments) and the final sample counts."""
     cs, need_n, nconv = pre
@@ -106,6 +106,19 @@ def simulate(pre, budget, phase_slots=1 << 23, mstep=0.25, kmin_first=True, floo
             break
         nw = n[want_pix]
         need = need_n[want_pix, nw].astype(np.float64)
+        if pool:  # the prediction pooled over the pixel's 3x3 neighbourhood (each at its own n)
+            cur = need_n[np.arange(npix), np.maximum(n, 1)].astype(np.float64).reshape(-1, width)
+            cur[(n == 0).reshape(-1, width)] = np.nan
+            pad = np.pad(cur, 1, constant_values=np.nan)
+            h, w_ = cur.shape
+            stack = np.stack([pad[dy:dy + h, dx:dx + w_] for dy in range(3) for dx in range(3)])
+            if pool == 2:
+                pooled = np.nanmedian(stack, axis=0)
+            else:
+                wts = np.ones(9); wts[4] = pool_w
+                ok = ~np.isnan(stack)
+                pooled = np.nansum(stack * wts[:, None, None], axis=0) / np.sum(ok * wts[:, None, None], axis=0)
+            need = pooled.reshape(-1)[want_pix]
         left = budget - nw
         margin = (1.0 + mstep * (g - 1)) if margins is None else margins[min(g - 1, len(margins) - 1)]
         want = (need - nw) * margin
@@ -114,7 +127,9 @@ def simulate(pre, budget, phase_slots=1 << 23, mstep=0.25, kmin_first=True, floo
         kb = np.maximum(kb, lo)
         kb = (kb + 3) & ~3
         kb = np.minimum(kb, np.minimum(left, kcap))
-        if floor and g + 1 >= floor_from and (floor != "if_small" or int(kb.sum()) < phase_slots):  # k_adapt_floor
+        if finish_slots is not None and int(np.minimum(left, kcap).sum() - kb.sum()) < finish_slots:
+            kb = np.minimum(left, kcap)  # finishing every pixel now costs less than another phase
+        elif floor and g + 1 >= floor_from and (floor != "if_small" or int(kb.sum()) < phase_slots):  # k_adapt_floor
             na = int((kb != 0).sum())
             km = -(-phase_slots // max(na, 1))
             kb = np.where(kb != 0, np.minimum((np.maximum(kb, np.minimum(km, left)) + 3) & ~3, np.minimum(left, kcap)), 0)
@@ -123,11 +138,11 @@ def simulate(pre, budget, phase_slots=1 << 23, mstep=0.25, kmin_first=True, floo
     return phases, n
 
 
-def cost(phases, rate=6.6e9, drain=0.36e-3, per_phase=0.1e-3, first=2.2e-3):
-    """Frame time model fitted to a measured C3 frame (profiles/r05 r8a trace: phase launches of
-    16.2 / 51.9 / 12.4 M segments in 2.20 / 8.24 / 2.24 ms): phases after the first at a
-    segment rate plus a fixed launch cost (drain), every phase with its record / expand / host
-    round trip; the first phase (cheaper segments: sky pixels) as measured."""
+def cost(phases, rate=8e9, drain=0.65e-3, per_phase=0.1e-3, first=2.2e-3):
+    """Frame time model fitted to measured C3 frames (kernel traces under profiles/r05): phases
+    after the first at a marginal segment rate plus a fixed launch cost (the launch's last paths
+    walking alone: phase 4's 1.6 M segments take 0.81 ms), every phase with its record / expand /
+    host round trip; the first phase (cheaper segments: sky pixels) as measured."""
     t = first + per_phase + sum(p["traced"] / rate + drain + per_phase for p in phases[1:])
     rec = sum(p["recorded"] for p in phases)
     return t, rec / t / 1e6
@@ -142,24 +157,18 @@ def main():
     L, segs = samples(args.workload, args.cache, args.threads)
     budget = WORKLOADS[args.workload][3]
     pre = prepare(L, segs)
-    variants = {
-        "default": {},
-        "floor 2^22": dict(phase_slots=1 << 22),
-        "floor 2^24": dict(phase_slots=1 << 24),
-        "margin 0": dict(mstep=0.0),
-        "margin 0.5": dict(mstep=0.5),
-        "no floor": dict(floor=False),
-        "floor if small": dict(floor="if_small"),
-        "floor if small, no kmin": dict(floor="if_small", kmin_first=False),
-        "no floor, no kmin": dict(floor=False, kmin_first=False),
-        "if small,nokmin,m1.1": dict(floor="if_small", kmin_first=False, margins=[1.0, 1.1, 1.25]),
-        "if small,nokmin,m1.5": dict(floor="if_small", kmin_first=False, margins=[1.0, 1.5, 1.5]),
-        "if small,nokmin,2^22": dict(floor="if_small", kmin_first=False, phase_slots=1 << 22),
-        "if small,nokmin,2^21": dict(floor="if_small", kmin_first=False, phase_slots=1 << 21),
+    width = WORKLOADS[args.workload][2]
+    variants = {  # margins: the batch margin after phase 1, 2, 3+ (the kernel: margin1, then 1 + 0.25 (g - 1))
+        "round 4 (floor 2^23, own prediction)": dict(phase_slots=1 << 23, margins=[1.0, 1.25, 1.5]),
+        "floor 2^20, own prediction": dict(phase_slots=1 << 20, margins=[1.0, 1.25, 1.5]),
+        "default (floor 2^21, margin 0.8, pooled x8)": dict(phase_slots=1 << 21, margins=[0.8, 1.25, 1.5], pool=1,
+                                                             pool_w=8.0, width=width),
+        "default + finish below 2^22 slots": dict(phase_slots=1 << 21, margins=[0.8, 1.25, 1.5], pool=1, pool_w=8.0,
+                                                   width=width, finish_slots=1 << 22),
     }
     for name, kw in variants.items():
         phases, n = simulate(pre, budget, **kw)
-        t, v = cost(phases)
+        t, v = cost(phases, drain=0.65e-3, rate=8e9)
         tr = sum(p["traced"] for p in phases)
         rc = sum(p["recorded"] for p in phases)
         desc = "; ".join(f"p{p['phase']} {p['pixels']} px {p['slots'] / 1e6:.2f}M slots {p['traced'] / 1e6:.1f}M tr "

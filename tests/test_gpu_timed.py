@@ -184,7 +184,8 @@ def test_adaptive_recorded_segments_equal_oracle(rtx_mod, orc, scenes, acase, ro
 FULL_BUDGET_CASES = [(1, 200, 0.7), (3, 2048, 0.5)]  # bench case index, spp, band row (fraction of H)
 TUNES = {"phases": {}, "phases_small": dict(phase_slots=4096, phase_kcap=8),
          "phases_kcap4": dict(phase_slots=64, phase_kcap=4), "phases_first_uniform": dict(first_map=0),
-         "phases_floor_2e23": dict(phase_slots=1 << 23)}
+         "phases_floor_2e23": dict(phase_slots=1 << 23),
+         "phases_unpooled": dict(margin1=1.0, pool_w=0.0)}
 
 
 @pytest.mark.parametrize("tune", sorted(TUNES))
