@@ -76,7 +76,7 @@ def prepare(L, segs):
 
 def simulate(pre, budget, phase_slots=1 << 23, mstep=0.25, kmin_first=True, floor=True, min_batch=(4, 4),
              first=MIN_SPP, kcap=None, margins=None, floor_from=2, pool=0, width=None, pool_w=1.0,
-             finish_slots=None):
+             finish_slots=None, pool_r=1):
     """Replays the phase policy; returns per-phase dicts (pixels, slots, traced and recorded
     segments) and the final sample counts."""
     cs, need_n, nconv = pre
@@ -109,13 +109,14 @@ def simulate(pre, budget, phase_slots=1 << 23, mstep=0.25, kmin_first=True, floo
         if pool:  # the prediction pooled over the pixel's 3x3 neighbourhood (each at its own n)
             cur = need_n[np.arange(npix), np.maximum(n, 1)].astype(np.float64).reshape(-1, width)
             cur[(n == 0).reshape(-1, width)] = np.nan
-            pad = np.pad(cur, 1, constant_values=np.nan)
+            R = pool_r
+            pad = np.pad(cur, R, constant_values=np.nan)
             h, w_ = cur.shape
-            stack = np.stack([pad[dy:dy + h, dx:dx + w_] for dy in range(3) for dx in range(3)])
+            stack = np.stack([pad[dy:dy + h, dx:dx + w_] for dy in range(2 * R + 1) for dx in range(2 * R + 1)])
             if pool == 2:
                 pooled = np.nanmedian(stack, axis=0)
             else:
-                wts = np.ones(9); wts[4] = pool_w
+                wts = np.ones(stack.shape[0]); wts[stack.shape[0] // 2] = pool_w
                 ok = ~np.isnan(stack)
                 pooled = np.nansum(stack * wts[:, None, None], axis=0) / np.sum(ok * wts[:, None, None], axis=0)
             need = pooled.reshape(-1)[want_pix]
