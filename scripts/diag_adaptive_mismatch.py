@@ -16,6 +16,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "3360-ray-tracer_amd"))
 import bench  # noqa: E402  (WORKLOADS, adaptive constants)
 import oracle_ctypes as orc  # noqa: E402
