@@ -126,7 +126,13 @@ struct BandSink {
   int64_t align;
   int (*copy)(void* ctx, int64_t p0, int64_t p1, hipStream_t cs);
   void* ctx;
+  // Adaptive renders: the caller's whole-image host framebuffer as the device sees it (pinned,
+  // mapped), or nullptr.  With it, the output goes to the host early, while the last phases
+  // still run (copy stream), and the pixels those phases change are written into it by the
+  // device at the end (k_patch_host) instead of a second whole-frame copy.
+  double* host_rgb_dev = nullptr;
 };
+constexpr int64_t kEarlyOutDiv = 4;  // the early output once a phase holds at most npix / 4 pixels
 constexpr int kBands = 8;  // bands of the last accumulate and of the D2H copies that overlap them (ab_bands_*: 2 / 4 / 8 / 16)
 
 // Adaptive renders in phases (render_adaptive)
@@ -195,6 +201,7 @@ struct rtx_scene {
   // render workspace (grow-only)
   DevBuf px_sum, px_mean, px_m2, px_samples, px_conv, lbuf, queue[2], counters, out_rgb, out_spp, rays, hits;
   DevBuf p3_scratch, p3_body;  // device P3 encoding (rtx_p3.h)
+  DevBuf patch_q;              // adaptive early output: the pixels still sampling when it went
   HostBuf stage_rgb, stage_spp;  // rtx_render_multi: pinned D2H staging of this device's stripes
   HostBuf counters_h;            // timed renders: pinned copy of the statistics counters (read after the end event)
   // ev[0] / ev[1]: a timed render's start and end (rtx_stats.kernel_ms), ev[2] / ev[3]: the
@@ -215,7 +222,7 @@ struct rtx_scene {
     (void)hipSetDevice(device);
     for (DevBuf* b : {&nodes, &prims, &mats, &texs, &images, &fnodes, &tri_n, &px_sum, &px_mean, &px_m2, &px_samples,
                       &px_conv, &lbuf, &queue[0], &queue[1], &counters, &out_rgb, &out_spp, &rays, &hits, &p3_scratch,
-                      &p3_body, &calib_rgb})
+                      &p3_body, &calib_rgb, &patch_q})
       b->release();
     for (auto& t : texels) t.release();
     stage_rgb.release(), stage_spp.release();
@@ -748,9 +755,9 @@ int set_segbuf(unsigned long long* ctr, uint16_t* segs, hipStream_t st) {
 // or stop; every phase is a launch of its own with its own drain.
 // `mark` records a hot-kernel timing event (before and after each persistent launch);
 // hot_launches counts them.  The caller resolves the pixels (k_resolve).
-template <class Mark>
+template <class Mark, class Early>
 int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const rtx_render_params* prm,
-                    const PixelSoA& px, int budget, hipStream_t s, Mark mark, uint64_t& hot_launches) {
+                    const PixelSoA& px, int budget, hipStream_t s, Mark mark, uint64_t& hot_launches, Early early) {
   const int64_t npix = A.npix;
   const int K1 = std::min(std::max(1, prm->min_spp), budget);
   static const bool debug = std::getenv("RTX_DEBUG_ADAPT") != nullptr;  // per-phase slot counts on stderr
@@ -896,6 +903,9 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
     const unsigned long long nsl = ((const volatile unsigned long long*)w.total_h.p)[0];
     const int64_t active = (int64_t)((const volatile unsigned long long*)w.total_h.p)[1];
     if (nsl == 0) break;
+    // the output once few pixels are left: every other pixel is final (phase g's list holds the
+    // rest, and later phases' lists are subsets of it)
+    if ((rc = early(g, active, w.lst[g & 1].as<uint32_t>()))) return rc;
     if ((rc = launch(g, Lg, Ag, w.segs.as<uint16_t>(), active))) return rc;
     if ((rc = record(g, Ag.L, active))) return rc;
   }
@@ -1322,7 +1332,8 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     if (g_debug_host) g_t_launch = host_us();
   }
   const bool banded = sum_path && sink && npix > 0;
-  if (banded) {
+  const bool early_ok = phased && sink && sink->host_rgb_dev && npix > 0;
+  if (banded || early_ok) {
     if (!sc->copy_stream) HIPC(hipStreamCreateWithFlags(&sc->copy_stream, hipStreamNonBlocking));
     while (sc->band_ev.size() < kBands + 1) {
       hipEvent_t e = nullptr;
@@ -1380,6 +1391,27 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   if (timed) HIPC(hipEventRecord(sc->ev[0], s));
   const int pix_blocks = (int)((npix + kBlock - 1) / kBlock);
   const int wf_grid = std::max(1, std::min<int>(sc->cus * 16, (int)((nslots + kBlock - 1) / kBlock)));
+  // Adaptive early output: once a phase holds at most npix / kEarlyOutDiv pixels, every other
+  // pixel is final, so the whole output is resolved and copied to the host on the copy stream
+  // while the remaining phases run; at the end the device writes only that phase's pixels into
+  // the host framebuffer (k_patch_host).  (The copy engine does not need the CUs the phase
+  // launches hold.)
+  int64_t patch_n = -1;
+  auto early = [&](int g, int64_t active, const uint32_t* list) -> int {
+    (void)g;
+    if (!early_ok || patch_n >= 0 || active * kEarlyOutDiv > npix) return RTX_OK;
+    int rc2;
+    if ((rc2 = sc->patch_q.reserve((size_t)std::max<int64_t>(1, active) * sizeof(uint32_t)))) return rc2;
+    hipLaunchKernelGGL(k_resolve, dim3(pix_blocks), dim3(kBlock), 0, s, px, npix, 0, prm->spp, d_rgb, d_spp);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(sc->patch_q.p, list, (size_t)active * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    HIPC(hipEventRecord(sc->band_ev[0], s));
+    HIPC(hipStreamWaitEvent(sc->copy_stream, sc->band_ev[0], 0));
+    if ((rc2 = sink->copy(sink->ctx, 0, npix, sc->copy_stream))) return rc2;
+    HIPC(hipEventRecord(sc->band_ev[1], sc->copy_stream));
+    patch_n = active;
+    return RTX_OK;
+  };
   if (phased) {
     if ((rc = render_adaptive(sc, L, A, prm, px, budget, s, [&](hipStream_t st) -> int {
            if (timed) {
@@ -1388,8 +1420,17 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
              HIPC(hipEventRecord(e, st));
            }
            return RTX_OK;
-         }, hot_launches)))
+         }, hot_launches, early)))
       return rc;
+    if (patch_n >= 0) {  // the early copy is done before the device patches the same framebuffer
+      HIPC(hipStreamWaitEvent(s, sc->band_ev[1], 0));
+      if (patch_n > 0) {
+        hipLaunchKernelGGL(k_patch_host, dim3((unsigned)((patch_n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, px,
+                           npix, sc->patch_q.as<uint32_t>(), patch_n, map, sink->host_rgb_dev, d_rgb, d_spp);
+        HIPC(hipGetLastError());
+      }
+      resolved = true;
+    }
   }
   for (int s0 = 0, Kc = 0; s0 < budget && !phased; s0 += Kc) {
     Kc = std::min(K, budget - s0);
@@ -1474,7 +1515,7 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   if (timed) HIPC(hipEventRecord(sc->ev[1], s));
   // renders the accumulate does not band (adaptive sampling): the whole output to the sink here,
   // on the stream before the event the host waits on, so one host wait covers the frame and its copy
-  if (sink && !banded && npix > 0) {
+  if (sink && !banded && npix > 0 && patch_n < 0) {
     if ((rc = sink->copy(sink->ctx, 0, npix, s))) return rc;
   }
   if (timed) {  // the statistics come back with the frame: one wait, no blocking copy after it
@@ -1610,7 +1651,12 @@ int render_stripes_to_host(rtx_scene* sc, const rtx_camera* cam, const rtx_rende
                           src + (size_t)rs * k.W * 3, (size_t)(r1 - rs) * k.row_rgb, hipMemcpyDeviceToHost, cs));
     return RTX_OK;
   };
-  const BandSink sink{R * W, copy, &ctx};
+  BandSink sink{R * W, copy, &ctx};
+  if (direct) {  // adaptive renders may write their last pixels straight into the caller's pinned rows
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, out_rgb, 0) == hipSuccess) sink.host_rgb_dev = (double*)dp;
+    else (void)hipGetLastError();
+  }
   if ((rc = render_device_impl(sc, cam, &q, sc->out_rgb.as<double>(), sc->out_spp.as<int32_t>(), st, sc->stream,
                                &sink)))
     return rc;

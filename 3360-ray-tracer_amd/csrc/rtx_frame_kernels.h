@@ -649,6 +649,27 @@ __global__ void k_slot_block_init(unsigned long long* __restrict__ ctr, int set,
   if (i < kSpread) ctr[kSpreadBase + i * kSpreadStride] = 0ull;
   if (i == 0 && set) ctr[8 * 16] = nslots, ctr[8 * 16 + 2] = smap;
 }
+// The pixels an adaptive frame kept sampling after its output went to the host early
+// (render_device_impl): each one's final value (k_resolve's arithmetic, adaptive) written
+// straight into the caller's host framebuffer (device-mapped pinned memory, the whole image,
+// pixel (x, y) at y * W + x) and into the device output.
+__global__ __launch_bounds__(kBlock) void k_patch_host(PixelSoA px, int64_t npix, const uint32_t* __restrict__ list,
+                                                       int64_t n, PixelMap map, double* __restrict__ host_rgb,
+                                                       double* __restrict__ rgb, int32_t* __restrict__ spp_out) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const int64_t p = list[i];
+  const int ns = px.samples[p];
+  const double sc = ns > 0 ? 1.0 / (double)(float)ns : 0.0;
+  int x, y;
+  map.xy((uint32_t)p, x, y);
+  double* h = host_rgb + 3 * ((int64_t)y * map.W + x);
+  for (int c = 0; c < 3; c++) {
+    const double v = ns > 0 ? sc * px.sum[c * npix + p] : 0.0;
+    rgb[3 * p + c] = v, h[c] = v;
+  }
+  if (spp_out) spp_out[p] = ns;
+}
 __global__ __launch_bounds__(kBlock) void k_resolve(PixelSoA px, int64_t npix, int megakernel, int spp,
                                                     double* __restrict__ rgb, int32_t* __restrict__ spp_out) {
   // megakernel: 1 = DefaultSampler (divide by spp), 2 = AdaptiveSampler (by the pixel's count)

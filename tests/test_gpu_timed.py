@@ -385,6 +385,33 @@ def test_render_multi_banded_output_one_device(rtx_mod, scenes):
             assert st["rays_total"] == fst["rays_total"]
 
 
+def test_render_multi_adaptive_early_output_into_pinned_buffer(rtx_mod, scenes):
+    """The benchmark's adaptive path: once a phase holds at most a quarter of the pixels, the
+    output goes to the pinned caller framebuffer early (copy stream) and the device writes the
+    remaining pixels' final values into it at the end (k_patch_host).  Against rtx_render (no
+    sink, one resolve at the end): same bytes and sample counts, for one device and for two
+    (interleaved stripes), with the default phases and with forced small ones."""
+    import torch
+
+    path, d = scenes("bunny")
+    cam = rtx_mod.camera(rtx_mod.camera_config("c3_bunny", width=120))
+    npix = cam.image_width * cam.image_height
+    other = rtx_mod.DeviceScene(rtx_mod.HostScene.load(path))
+    for knobs in ({}, dict(phase_slots=64, phase_kcap=8)):
+        try:
+            rtx_mod.adapt_tune(**knobs)
+            full, fsp, _ = d.render(cam, 200, 20, seed=33, adaptive=True, mode="persistent", precision="fast")
+            for group in ([d], [d, other]):
+                pinned = torch.full((npix, 3), -1.0, dtype=torch.float64).pin_memory()
+                out = pinned.numpy()
+                rgb, sp, st, _ = rtx_mod.render_multi(group, cam, 200, 20, seed=33, adaptive=True, mode="persistent",
+                                                      precision="fast", out=out)
+                assert np.array_equal(out, full) and np.array_equal(sp, fsp), (knobs, len(group))
+                assert (fsp < 200).any() and (fsp > 16).any()  # phases past the first ran
+        finally:
+            rtx_mod.adapt_tune()
+
+
 def test_render_multi_rejects_bad_arguments(rtx_mod, scenes):
     _, d = scenes("final")
     cam = rtx_mod.camera(rtx_mod.camera_config("c2_final", width=16))
