@@ -76,7 +76,7 @@ def prepare(L, segs):
 
 def simulate(pre, budget, phase_slots=1 << 23, mstep=0.25, kmin_first=True, floor=True, min_batch=(4, 4),
              first=MIN_SPP, kcap=None, margins=None, floor_from=2, pool=0, width=None, pool_w=1.0,
-             finish_slots=None, pool_r=1):
+             finish_slots=None, pool_r=1, capture=None):
     """Replays the phase policy; returns per-phase dicts (pixels, slots, traced and recorded
     segments) and the final sample counts."""
     cs, need_n, nconv = pre
@@ -91,6 +91,8 @@ def simulate(pre, budget, phase_slots=1 << 23, mstep=0.25, kmin_first=True, floo
         if act.size == 0:
             break
         kk, n0 = k[act], n[act]
+        if capture is not None:  # the phase's pixels, first sample and batch (scripts: drain studies)
+            capture.append((act.copy(), n0.copy(), kk.copy()))
         traced = int((cs[act, n0 + kk] - cs[act, n0]).sum())
         nc = nconv[act]
         nn = np.where(nc <= n0 + kk, nc, n0 + kk)
