@@ -81,9 +81,12 @@ struct RenderArgs {
 // Pixel-major: the path-end writes of neighbouring lanes (same pixel, consecutive samples)
 // are contiguous.  (Sample-major [k][c][p] coalesces the accumulate's reads but scatters
 // these writes: A/B r01 -2 % C2 and bunny.)
+// Stored non-temporal (global_store ... nt): the records (2.7 GB per C3 frame) stream through
+// the L2 instead of displacing the scene's nodes and primitives (C3 +1.5 %, C3 adaptive +0.9 %,
+// C2 +-0; profiles/r05/ab/ab_nt_records_r9c.txt).
 __device__ __forceinline__ void store_radiance(const RenderArgs& A, uint32_t slot, V3 L) {
   double* Lp = A.L + 3 * (uint64_t)slot;
-  Lp[0] = L.x, Lp[1] = L.y, Lp[2] = L.z;
+  __builtin_nontemporal_store(L.x, Lp), __builtin_nontemporal_store(L.y, Lp + 1), __builtin_nontemporal_store(L.z, Lp + 2);
 }
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
