@@ -25,7 +25,7 @@ constexpr int kBlock = 256;
 constexpr int kTraceWaves = 4;  // min waves per SIMD for the trace kernels (<= 128 VGPRs; 3 and 5 slower)
 constexpr int kSlotTargetLog2 = 29;  // persistent: up to 2^29 slots (pixel x sample) per launch (r02: 2^29 vs 2^27 C4 +4.0 %, C5 +1.3 %), capped by free memory
 constexpr int kRefillMin = 24;      // persistent lanes: refill once this many lanes of a wave are idle (ab_refill2_*)
-constexpr int kRefillMinPark = 16;  // the same for the PARK kernel
+constexpr int kRefillMinPark = 12;  // the same for the PARK kernel (12 vs 16: C3 adaptive +0.5 %, fixed +-0; r9f / r9g)
 constexpr int kParkAt = 16;  // PARK kernel: park traversals once at most this many lanes still walk (ab_parkT_*)
 // persistent: slots taken per atomic on a region's slot counter, by schedule (k_persistent
 // kChunk): the plain kernel 256 (ab_chunk_*; 512 C2 -0.4 %), the PARK kernel 512 (bunny C3
