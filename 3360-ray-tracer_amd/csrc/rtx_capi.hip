@@ -132,7 +132,7 @@ struct BandSink {
   // device at the end (k_patch_host) instead of a second whole-frame copy.
   double* host_rgb_dev = nullptr;
 };
-constexpr int64_t kEarlyOutDiv = 4;  // the early output once a phase holds at most npix / 4 pixels
+constexpr int64_t kEarlyOutDiv = 32;  // the early output once a phase holds at most npix / 32 pixels (4: C3 / C4 adaptive -0.7 %, r9j / r9k)
 constexpr int kBands = 8;  // bands of the last accumulate and of the D2H copies that overlap them (ab_bands_*: 2 / 4 / 8 / 16)
 
 // Adaptive renders in phases (render_adaptive)
