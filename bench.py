@@ -136,6 +136,9 @@ def main():
     ap.add_argument("--adapt-tune", default="",
                     help="tuning of the adaptive phases (rtx.adapt_tune), e.g. phase_slots=4194304,phase_mstep=0.5 "
                          "(never changes results, only the work)")
+    ap.add_argument("--min-spp", type=int, default=ADAPTIVE_MIN_SPP,
+                    help="adaptive renders: samples of the first pass (the reference's 16; = spp runs the phase "
+                         "kernel over exactly the fixed-spp frame's samples, an overhead experiment)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-adaptive-leg", action="store_true",
                     help="skip the adaptive-sampling frames timed beside a fixed-spp line")
@@ -187,7 +190,7 @@ def main():
         p = rtx.RenderParams()
         p.spp, p.max_depth, p.seed = spp, depth, args.seed
         p.adaptive = int(args.adaptive if adaptive is None else adaptive)
-        p.min_spp, p.rel_threshold = ADAPTIVE_MIN_SPP, ADAPTIVE_REL
+        p.min_spp, p.rel_threshold = args.min_spp, ADAPTIVE_REL
         p.mode, p.precision = rtx.MODES[args.mode], rtx.PRECISIONS[args.precision]
         p.stripe_rows, p.stripe_index, p.stripe_count = STRIPE_ROWS, rank, world
         p.flags = flags | (rtx.RTX_FLAG_GENERIC if generic else 0)

@@ -608,6 +608,12 @@ inline V3 mat_emitted(const Scene& S, const Material& m, double u, double v, V3 
   return {0, 0, 0};                                                 // material.h:50-54
 }
 
+// Deliberate estimator changes for the statistical parity leg's power check
+// (tests/test_statistical_parity.py): 0 (always, except in that check) is the reference's
+// estimator; 1 scales the Lambertian BRDF by 0.98, 2 brightens the sky by 2 %, 3 drops the
+// eta^2 factor of dielectric refraction (material.cc:246-253).  Set by orc_set_perturb.
+static int g_perturb = 0;
+
 inline double reflectance(double c, double ri) {  // material.cc:258-262
   double r0 = (1.0 - ri) / (1.0 + ri);
   r0 = r0 * r0;
@@ -625,6 +631,7 @@ bool mat_sample(const Scene& S, const Material& m, const Hit& rec, V3 wo, V3& wi
       pdf = (c <= 0.0f) ? 0.0f : (float)(c / kPi);
       if (dot(rec.normal, wi) <= 0) f = {0, 0, 0};  // Lambertian::Eval material.cc:36-46
       else f = tex_value(S, m.tex, rec.u, rec.v, rec.p) / kPi;
+      if (g_perturb == 1) f = 0.98 * f;
       return true;
     }
     case MAT_METAL: {
@@ -659,7 +666,7 @@ bool mat_sample(const Scene& S, const Material& m, const Hit& rec, V3 wo, V3& wi
         return true;
       }
       wi = refract(win, n, eta);
-      double k = eta * eta;
+      double k = g_perturb == 3 ? 1.0 : eta * eta;
       f = {k, k, k};
       return true;
     }
@@ -752,7 +759,8 @@ struct Camera {
 inline V3 sky(V3 d) {  // wavefront.cc:33-38
   V3 ud = normalize(d);
   double t = 0.5 * (ud.y + 1.0);
-  return (1.0 - t) * v3(1.0, 1.0, 1.0) + t * v3(0.5, 0.7, 1.0);
+  const V3 c = (1.0 - t) * v3(1.0, 1.0, 1.0) + t * v3(0.5, 0.7, 1.0);
+  return g_perturb == 2 ? 1.02 * c : c;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1222,6 +1230,12 @@ void* orc_scene_load(const char* file, const char* asset_dir) {
   return s;
 }
 void orc_scene_free(void* s) { delete (Scene*)s; }
+// the power check's deliberate estimator change (g_perturb); returns the previous setting
+int orc_set_perturb(int mode) {
+  const int old = g_perturb;
+  g_perturb = mode;
+  return old;
+}
 int orc_scene_counts(void* sp, int* nprims, int* nnodes, int* nmats, int* ntex) {
   Scene* s = (Scene*)sp;
   *nprims = (int)s->prims.size();

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Round 6 (r10a): the adaptive phase kernel (MAP 1, block-shared chunks) over exactly the fixed-spp
+# C3 frame's samples (adaptive with min_spp = spp = 200: one uniform first pass, nothing after it)
+# against the fixed-spp kernel (MAP 0): interleaved timing, then a PMC profile of each.
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+cd "$R"
+O=gpurun_out/r10a; mkdir -p $O
+B="--no-cpu-baseline --no-generic-leg --no-adaptive-leg --schedule park"
+for r in 1 2; do
+  timeout -k 10 200 python bench.py $B > $O/map0_$r.json 2> $O/map0_$r.err || { tail -20 $O/map0_$r.err; exit 1; }
+  timeout -k 10 200 python bench.py $B --adaptive --min-spp 200 > $O/map1u_$r.json 2> $O/map1u_$r.err || { tail -20 $O/map1u_$r.err; exit 1; }
+  python3 -c "
+import json
+for t in ('map0_$r', 'map1u_$r'):
+    d=json.loads(open('$O/'+t+'.json').read().strip().splitlines()[-1]); r=d['roofline']
+    print(t, round(d['value'],1), round(d['ms_per_step'],3), 'launch ms', round(r['avg_launch_ms'],3), 'launches/step', d['steps'] and None, 'nodes/seg', round(r['nodes_per_segment'],3), 'simd', r['simd_efficiency_nodes'], r['simd_efficiency_prims'])"
+done
+timeout -k 10 900 bash scripts/profile.sh r10a_map0 --schedule park || exit 1
+timeout -k 10 900 bash scripts/profile.sh r10a_map1u --schedule park --adaptive --min-spp 200 || exit 1
+echo done
