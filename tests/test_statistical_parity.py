@@ -23,7 +23,7 @@ false-alarm level of 1e-4, so a whole run of the 4 cases false-alarms below 0.2 
 Power: each case also renders the restatement with a deliberate 2 % estimator change (the
 Lambertian BRDF x 0.98; the sky x 1.02), which must fail.  (Two changes the review suggested are
 not estimator changes: Russian roulette's survival clamp only moves variance, since the
-survivors are divided by p, wavefront.cc:199-206; Schlick with eta instead of ref_idx_ gives the
+survivors are divided by p, wavefront.cc:188-206; Schlick with eta instead of ref_idx_ gives the
 same r0, ((1 - 1/n) / (1 + 1/n))^2 = ((n - 1) / (n + 1))^2.  Dropping refraction's eta^2
 factor, material.cc:252, mostly cancels between a path's entry and exit and is not detected
 at this size; the calibration file records its statistics.)
