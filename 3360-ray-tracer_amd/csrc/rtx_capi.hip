@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <atomic>
 #include <chrono>
 #include <numeric>
 #include <string>
@@ -152,6 +153,9 @@ struct AdaptTune {
   double pool_w;         // the pooled prediction's centre weight (< 0: kAdaptPoolW; 0: not pooled)
 };
 static AdaptTune g_tune{0, 0, -1, -1.0, -1.0, -1.0};
+// adaptive early outputs so far (renders whose output went to the host while phases still ran)
+// and the pixels k_patch_host rewrote: rtx_internal_early_output_stats, a test hook
+static std::atomic<long long> g_early_outputs{0}, g_early_patched{0};
 // render_adaptive: the margin of the batches after the first phase, and k_adapt_plan's centre
 // weight (0: each pixel's own prediction only): ranked first by scripts/adaptive_sim.py, then
 // C3 adaptive +4.0 %, C2 +0.5 % against the unpooled margin 1.0 (r05 r8j / r8k)
@@ -539,9 +543,10 @@ static int build_global_prims(const rtx_prim* prims, int64_t n, int32_t out[2]) 
 // The allowance of a scene's slot buffers (the radiance records of the samples in flight, the
 // wavefront's path queues, the adaptive workspaces): half of the device memory that is free or
 // already held by them, so several scenes on one device, or a smaller GPU, get smaller groups
-// instead of RTX_ERR_NOMEM.  ONE allowance for all of them: a render holds only its own kind's
-// buffers (render_device_impl releases the others when the kind changes) and sizes them
-// within the allowance minus what its other buffers take.  The free-memory query is made once
+// instead of RTX_ERR_NOMEM.  ONE allowance for all of them: a render keeps the other kinds'
+// buffers (and, for an adaptive render, the radiance buffer beyond its first pass) only while
+// they fit beside its own (render_device_impl releases them otherwise) and sizes its own within
+// the allowance minus what those kept buffers take.  The free-memory query is made once
 // per scene (the first render that sizes its slots; it costs ~0.5 ms, too much per frame):
 // scenes created later see what the earlier ones took.
 double slot_allowance(rtx_scene* sc) {
@@ -737,6 +742,13 @@ int persist_m(const Launch& L, const RenderArgs& A, unsigned long long* ns) {
 
 int time_park_schedule(rtx_scene* sc, const rtx_camera* cam, const rtx_render_params* prm, hipStream_t s);
 
+// Bytes of an adaptive render's uniform first pass (min_spp samples of every pixel): its
+// radiance records, and in counting renders their segment counts, in the scene's buffers.
+double adaptive_first_bytes(int64_t npix, const rtx_render_params* prm, int budget, bool count) {
+  const int K1 = std::min(std::max(1, prm->min_spp), budget);
+  return (double)npix * K1 * (3 * sizeof(double) + (count ? 2 : 0));
+}
+
 // Counting renders: the persistent launch's slot counter block names the buffer its paths'
 // segment counts go to (k_persistent COUNT builds read word 8 * 16 + 4 of it).
 int set_segbuf(unsigned long long* ctr, uint16_t* segs, hipStream_t st) {
@@ -757,7 +769,8 @@ int set_segbuf(unsigned long long* ctr, uint16_t* segs, hipStream_t st) {
 // hot_launches counts them.  The caller resolves the pixels (k_resolve).
 template <class Mark, class Early>
 int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const rtx_render_params* prm,
-                    const PixelSoA& px, int budget, hipStream_t s, Mark mark, uint64_t& hot_launches, Early early) {
+                    const PixelSoA& px, int budget, double other, hipStream_t s, Mark mark, uint64_t& hot_launches,
+                    Early early) {
   const int64_t npix = A.npix;
   const int K1 = std::min(std::max(1, prm->min_spp), budget);
   static const bool debug = std::getenv("RTX_DEBUG_ADAPT") != nullptr;  // per-phase slot counts on stderr
@@ -766,10 +779,11 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   AdaptWs& w = sc->aw;
   int rc;
   // the uniform first pass's radiance (and segment) records, in the scene's buffers
-  const double first_bytes = (double)npix * K1 * (3 * sizeof(double) + (L.count ? 2 : 0));
-  // slots after the first phase: 24 B of radiance + 8 B of slot map each (+ 2 B of segments)
-  const int64_t cap =
-      std::min<int64_t>(0xFFFFFFFFll, slot_target(sc, 32 + (L.count ? 2 : 0), 1ll << kSlotTargetLog2, first_bytes));
+  const double first_bytes = adaptive_first_bytes(npix, prm, budget, L.count);
+  // slots after the first phase: 24 B of radiance + 8 B of slot map each (+ 2 B of segments),
+  // within the allowance less the first pass and what the render keeps of other buffers
+  const int64_t cap = std::min<int64_t>(
+      0xFFFFFFFFll, slot_target(sc, 32 + (L.count ? 2 : 0), 1ll << kSlotTargetLog2, first_bytes + other));
   if (npix * 4 > cap) return fail(RTX_ERR_NOMEM, "adaptive render: too many pixels for the device memory");
   int32_t kcap = (int32_t)std::min<int64_t>(budget, std::max<int64_t>(4, (cap / npix) & ~3ll));
   if (g_tune.phase_kcap > 0) kcap = std::min(kcap, g_tune.phase_kcap);
@@ -1274,7 +1288,9 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
   // and what it needs itself fit in the allowance, and releases them only when they do not:
   // every release and reallocation synchronises the device, and frames that alternate kinds
   // (the bench's fixed-spp line, its adaptive leg, the CPU check) would pay it every time.
-  double other = 0.0;  // bytes of other kinds kept
+  // A phased render's first pass runs in the scene's radiance buffer (lbuf) at npix x min_spp
+  // slots: whatever a fixed-spp frame left there beyond that is kept like another kind's buffer.
+  double other = 0.0;  // bytes of other kinds kept (phased: and lbuf beyond the first pass)
   {
     const bool wf = prm->mode == RTX_MODE_WAVEFRONT;
     const double allow = slot_allowance(sc);
@@ -1282,9 +1298,12 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     const double want = per_slot * (double)npix * (double)std::max(1, budget);
     const double aw_bytes = (double)sc->aw.lbuf.n + (double)sc->aw.smap.n + (double)sc->aw.segs.n;
     const double queue_bytes = (double)sc->queue[0].n + (double)sc->queue[1].n;
-    other = (phased ? 0.0 : aw_bytes) + (wf ? 0.0 : queue_bytes);
+    const double first_bytes = phased ? adaptive_first_bytes(npix, prm, budget, L.count) : 0.0;
+    const double lbuf_extra = phased ? std::max(0.0, (double)sc->lbuf.n - first_bytes) : 0.0;
+    other = (phased ? lbuf_extra : aw_bytes) + (wf ? 0.0 : queue_bytes);
     if (other + std::min(want, per_slot * (double)(1ll << kSlotTargetLog2)) > allow) {
       if (!phased) sc->aw.lbuf.release(), sc->aw.smap.release(), sc->aw.segs.release();
+      else if (lbuf_extra > 0.0) sc->lbuf.release();  // (render_adaptive reserves the first pass's size)
       if (!wf)
         for (auto& q : sc->queue) q.release();
       other = 0.0;
@@ -1410,24 +1429,33 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     if ((rc2 = sink->copy(sink->ctx, 0, npix, sc->copy_stream))) return rc2;
     HIPC(hipEventRecord(sc->band_ev[1], sc->copy_stream));
     patch_n = active;
+    g_early_outputs++, g_early_patched += active;
     return RTX_OK;
   };
   if (phased) {
-    if ((rc = render_adaptive(sc, L, A, prm, px, budget, s, [&](hipStream_t st) -> int {
+    if ((rc = render_adaptive(sc, L, A, prm, px, budget, other, s, [&](hipStream_t st) -> int {
            if (timed) {
              hipEvent_t e = ev_at(evi++);
              if (!e) return fail(RTX_ERR_HIP, "hipEventCreate failed");
              HIPC(hipEventRecord(e, st));
            }
            return RTX_OK;
-         }, hot_launches, early)))
+         }, hot_launches, early))) {
+      // an error after the early output was queued: the copy into the caller's framebuffer
+      // must be over before the caller gets the error (and may free or reuse the buffer)
+      if (patch_n >= 0) (void)hipEventSynchronize(sc->band_ev[1]);
       return rc;
+    }
     if (patch_n >= 0) {  // the early copy is done before the device patches the same framebuffer
-      HIPC(hipStreamWaitEvent(s, sc->band_ev[1], 0));
-      if (patch_n > 0) {
+      hipError_t e = hipStreamWaitEvent(s, sc->band_ev[1], 0);
+      if (e == hipSuccess && patch_n > 0) {
         hipLaunchKernelGGL(k_patch_host, dim3((unsigned)((patch_n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, px,
                            npix, sc->patch_q.as<uint32_t>(), patch_n, map, sink->host_rgb_dev, d_rgb, d_spp);
-        HIPC(hipGetLastError());
+        e = hipGetLastError();
+      }
+      if (e != hipSuccess) {
+        (void)hipEventSynchronize(sc->band_ev[1]);
+        return fail(RTX_ERR_HIP, std::string("adaptive early output: ") + hipGetErrorString(e));
       }
       resolved = true;
     }
@@ -1914,6 +1942,38 @@ extern "C" int rtx_internal_adapt_tune(int64_t phase_slots, int32_t phase_kcap, 
                                        double margin1, double pool_w) {
   if (phase_slots < 0 || phase_kcap < 0 || first_map > 1) return fail(RTX_ERR_INVALID, "bad tuning value");
   g_tune = AdaptTune{phase_slots, phase_kcap, first_map, phase_mstep, margin1, pool_w};
+  return RTX_OK;
+}
+
+// Test hook (not in rtx.h): the image rows of stripe `index` of `count` (stripe_rows-row
+// interleaved stripes) in the order the render writes them, through the same PixelMap the
+// kernels use (subset_pixels, PixelMap::xy): rows[0 .. *nrows).  No device needed.
+extern "C" int rtx_internal_stripe_rows(int32_t width, int32_t height, int32_t stripe_rows, int32_t index,
+                                        int32_t count, int32_t* rows, int64_t* nrows) {
+  if (!rows || !nrows) return fail(RTX_ERR_INVALID, "NULL argument");
+  rtx_camera cam{};
+  cam.image_width = width, cam.image_height = height;
+  rtx_render_params prm{};
+  prm.stripe_rows = stripe_rows, prm.stripe_index = index, prm.stripe_count = count;
+  PixelMap m;
+  std::string err;
+  const int64_t n = subset_pixels(&cam, &prm, m, err);
+  if (n < 0) return fail(RTX_ERR_INVALID, err);
+  *nrows = m.h;
+  for (int r = 0; r < m.h; r++) {
+    int x, y;
+    m.xy((uint32_t)r * (uint32_t)m.w, x, y);
+    rows[r] = y;
+  }
+  return RTX_OK;
+}
+
+// Test hook (not in rtx.h): how many adaptive renders of this process sent their output to the
+// host early (while phases still ran; render_device_impl `early`), and how many pixels the
+// device patched afterwards (k_patch_host), summed over them.
+extern "C" int rtx_internal_early_output_stats(long long* outputs, long long* patched) {
+  if (!outputs || !patched) return fail(RTX_ERR_INVALID, "NULL argument");
+  *outputs = g_early_outputs.load(), *patched = g_early_patched.load();
   return RTX_OK;
 }
 

@@ -39,8 +39,8 @@ struct PixelMap {
   int32_t stripes;  // 0: rectangle, 1: stripes
   int32_t x0, y0, w, h;
   int32_t srows, sidx, scount;
-  // 32-bit arithmetic: the host keeps pixel counts below 2^31
-  __device__ __forceinline__ void xy(uint32_t local, int& x, int& y) const {
+  // 32-bit arithmetic: the host keeps pixel counts below 2^31 (host side: rtx_internal_stripe_rows)
+  __host__ __device__ __forceinline__ void xy(uint32_t local, int& x, int& y) const {
     if (!stripes) {
       const uint32_t r = local / (uint32_t)w;
       x = x0 + (int)(local - r * (uint32_t)w);

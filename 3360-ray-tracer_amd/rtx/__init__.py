@@ -367,6 +367,18 @@ def adapt_tune(phase_slots=0, phase_kcap=0, first_map=-1, phase_mstep=-1.0, marg
     _check(f(phase_slots, phase_kcap, first_map, phase_mstep, margin1, pool_w), "rtx_internal_adapt_tune")
 
 
+def early_output_stats():
+    """Test hook (rtx_internal_early_output_stats, not in rtx.h): (adaptive renders of this
+    process whose output went to the host while phases still ran, pixels the device patched
+    into the host framebuffer afterwards)."""
+    f = lib().rtx_internal_early_output_stats
+    f.argtypes = [C.POINTER(C.c_longlong), C.POINTER(C.c_longlong)]
+    f.restype = C.c_int
+    a, b = C.c_longlong(), C.c_longlong()
+    _check(f(C.byref(a), C.byref(b)), "rtx_internal_early_output_stats")
+    return a.value, b.value
+
+
 def render_multi(scenes, cam, spp, max_depth, seed=1234, adaptive=True, mode="persistent", precision="fast",
                  stripe_rows=8, stripe_index=0, stripe_count=0, out=None, schedule=None, min_spp=16,
                  rel_threshold=float(np.float32(0.05)), samples_per_group=0):
@@ -436,9 +448,17 @@ def bvh_build(bounds, device=0, on="gpu"):
     return nodes[:nn.value], idx[:n]
 
 
-def stripe_rows_of(height, stripe_rows, index, count):
-    """Rows owned by stripe `index` (interleaved row stripes), in output order."""
-    return [y for y in range(height) if (y // stripe_rows) % count == index]
+def stripe_rows_of(height, stripe_rows, index, count, width=1):
+    """Rows owned by stripe `index` (interleaved row stripes), in output order: the library's own
+    pixel map (rtx_internal_stripe_rows: subset_pixels + PixelMap::xy, host side, no device)."""
+    f = lib().rtx_internal_stripe_rows
+    f.argtypes = [C.c_int32] * 5 + [C.c_void_p, C.POINTER(C.c_int64)]
+    f.restype = C.c_int
+    rows = np.zeros(max(1, height), np.int32)
+    n = C.c_int64()
+    _check(f(width, height, stripe_rows, index, count, rows.ctypes.data_as(C.c_void_p), C.byref(n)),
+           "rtx_internal_stripe_rows")
+    return [int(y) for y in rows[:n.value]]
 
 
 def write_ppm(path, rgb, width, height):

@@ -386,11 +386,12 @@ def test_render_multi_banded_output_one_device(rtx_mod, scenes):
 
 
 def test_render_multi_adaptive_early_output_into_pinned_buffer(rtx_mod, scenes):
-    """The benchmark's adaptive path: once a phase holds at most a quarter of the pixels, the
-    output goes to the pinned caller framebuffer early (copy stream) and the device writes the
+    """The benchmark's adaptive path: once a phase holds at most npix / 32 pixels (kEarlyOutDiv),
+    the output goes to the pinned caller framebuffer early (copy stream) and the device writes the
     remaining pixels' final values into it at the end (k_patch_host).  Against rtx_render (no
     sink, one resolve at the end): same bytes and sample counts, for one device and for two
-    (interleaved stripes), with the default phases and with forced small ones."""
+    (interleaved stripes), with the default phases and with forced small ones; the early output
+    must have fired, with pixels patched, for the forced small phases."""
     import torch
 
     path, d = scenes("bunny")
@@ -402,12 +403,16 @@ def test_render_multi_adaptive_early_output_into_pinned_buffer(rtx_mod, scenes):
             rtx_mod.adapt_tune(**knobs)
             full, fsp, _ = d.render(cam, 200, 20, seed=33, adaptive=True, mode="persistent", precision="fast")
             for group in ([d], [d, other]):
+                n0, p0 = rtx_mod.early_output_stats()
                 pinned = torch.full((npix, 3), -1.0, dtype=torch.float64).pin_memory()
                 out = pinned.numpy()
                 rgb, sp, st, _ = rtx_mod.render_multi(group, cam, 200, 20, seed=33, adaptive=True, mode="persistent",
                                                       precision="fast", out=out)
                 assert np.array_equal(out, full) and np.array_equal(sp, fsp), (knobs, len(group))
                 assert (fsp < 200).any() and (fsp > 16).any()  # phases past the first ran
+                n1, p1 = rtx_mod.early_output_stats()
+                if knobs:  # small phases: many phases, the last ones few pixels -> early output, patched
+                    assert n1 - n0 == len(group) and p1 > p0, (n0, n1, p0, p1)
         finally:
             rtx_mod.adapt_tune()
 

@@ -1,7 +1,10 @@
-"""N>1 path on CPU: world_size-2 `gloo` ranks, each rendering its interleaved row stripes
-(the bench's partition) with the CPU oracle; the gathered image must equal the
-single-process render bit for bit (the RNG is keyed by the global pixel), and the
-max-over-ranks timing reduction must pick the slowest rank."""
+"""N>1 path on CPU: world_size-2 `gloo` ranks, each rendering the rows of its interleaved row
+stripes (the bench's partition) as the PRODUCT's pixel map assigns them
+(rtx.stripe_rows_of -> rtx_internal_stripe_rows: the library's subset_pixels + PixelMap::xy,
+host side) with the CPU oracle; the gathered image must equal the single-process render bit for
+bit (the RNG is keyed by the global pixel), and the max-over-ranks timing reduction must pick the
+slowest rank.  The pixel map itself is checked against its closed form for every size and rank
+count the bench can use."""
 import os
 import socket
 
@@ -27,20 +30,23 @@ def free_port():
 
 
 def stripe_rows(h, rows, idx, count):
+    """Closed form of the interleaved stripes (stripe k -> rank k mod count)."""
     return [y for y in range(h) if (y // rows) % count == idx]
 
 
 def worker(rank, world, port, out_dir):
     import sys
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "3360-ray-tracer_amd"))
     import oracle_ctypes as orc
+    import rtx
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     cfg = orc.camera_preset("c2_final")
     s = orc.Scene(scene_path("final"))
     H = orc.make_camera(cfg, W).height
-    rows = stripe_rows(H, STRIPE_ROWS, rank, world)
+    rows = rtx.stripe_rows_of(H, STRIPE_ROWS, rank, world, width=W)  # the product's pixel map
     mine = np.zeros((H, W, 3))
     for y in rows:  # contiguous rows of a stripe rendered as 1-row tiles
         fb, _, _ = s.render(cfg, W, SPP, DEPTH, SEED, adaptive=0, rng="philox", mode="per_pixel", tile=(0, y, W, 1))
@@ -69,10 +75,12 @@ def test_two_rank_stripes_match_single_process(tmp_path, orc):
     assert np.load(tmp_path / "tmax.npy")[0] == 2.0
 
 
-def test_stripes_cover_every_row_once():
-    for h in (1, 7, 36, 675, 2160):
+def test_stripes_cover_every_row_once(rtx_mod):
+    for h in (1, 7, 36, 562, 675, 2160):
         for n in (1, 2, 3, 4, 8):
-            rows = sorted(sum((stripe_rows(h, STRIPE_ROWS, k, n) for k in range(n)), []))
-            assert rows == list(range(h))
-            sizes = [len(stripe_rows(h, STRIPE_ROWS, k, n)) for k in range(n)]
+            per_rank = [rtx_mod.stripe_rows_of(h, STRIPE_ROWS, k, n, width=3840) for k in range(n)]
+            for k in range(n):  # the product's map is the closed form, in output order
+                assert per_rank[k] == stripe_rows(h, STRIPE_ROWS, k, n)
+            assert sorted(sum(per_rank, [])) == list(range(h))
+            sizes = [len(r) for r in per_rank]
             assert max(sizes) - min(sizes) <= STRIPE_ROWS  # balanced to within one stripe

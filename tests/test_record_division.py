@@ -2,7 +2,9 @@
 RecordSample's `delta / n` (pixel_state.h:30) formed from one reciprocal per sample and a
 Markstein correction must equal the IEEE quotient bit for bit.  A small C program (gcc,
 -ffp-contract=off, the C library's fma) checks random, integer-multiple and near-tie dividends
-for every count the budgets reach here (n <= 4096)."""
+for every count up to 4096, and for sampled larger counts up to 2^31 (every power of two and its
+neighbours, random counts between): the API accepts any spp budget, and the samples counter is
+32-bit."""
 import os
 import subprocess
 
@@ -22,11 +24,23 @@ static double div_by_count(double delta, double n, double y) {  /* as the kernel
   if (!(fabs(delta) >= 0x1p-900 && fabs(delta) < INFINITY)) q = delta / n;
   return q;
 }
+static long bad = 0, tot = 0;
+static void check_count(long n, int iters);
 int main(void) {
-  long bad = 0, tot = 0;
-  for (int n = 1; n <= 4096; n++) {
+  for (long n = 1; n <= 4096; n++) check_count(n, 1200);
+  for (int k = 12; k <= 31; k++)  /* powers of two and their neighbours up to 2^31 */
+    for (long d = -2; d <= 2; d++) {
+      const long n = (1L << k) + d;
+      if (n > 4096 && n <= (1L << 31)) check_count(n, 600);
+    }
+  for (int i = 0; i < 3000; i++) check_count(4097 + (long)(rnd() % ((1UL << 31) - 4096)), 200);
+  printf("checked %ld mismatches %ld\n", tot, bad);
+  return bad != 0;
+}
+static void check_count(long n, int iters) {
+  {
     const double dn = (double)n, y = 1.0 / dn;
-    for (int it = 0; it < 1200; it++) {
+    for (int it = 0; it < iters; it++) {
       double a;
       switch (it % 5) {
         case 0: a = bits((rnd() & 0x800FFFFFFFFFFFFFull) | ((uint64_t)(1023 - 40 + rnd() % 60) << 52)); break;
@@ -40,13 +54,11 @@ int main(void) {
       double q = div_by_count(a, dn, y), e = a / dn;
       tot++;
       if (!(isnan(q) && isnan(e)) && memcmp(&q, &e, 8) != 0) {
-        if (bad < 5) printf("n=%d a=%a got %a want %a\n", n, a, q, e);
+        if (bad < 5) printf("n=%ld a=%a got %a want %a\n", n, a, q, e);
         bad++;
       }
     }
   }
-  printf("checked %ld mismatches %ld\n", tot, bad);
-  return bad != 0;
 }
 """
 
