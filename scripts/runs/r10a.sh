@@ -18,4 +18,12 @@ for t in ('map0_$r', 'map1u_$r'):
 done
 timeout -k 10 900 bash scripts/profile.sh r10a_map0 --schedule park || exit 1
 timeout -k 10 900 bash scripts/profile.sh r10a_map1u --schedule park --adaptive --min-spp 200 || exit 1
+
+timeout -k 10 300 python -u -m pytest tests/test_gpu_timed.py -k "early_output or stripe" -x -q --timeout 200 --timeout-method thread > $O/pytest_early.log 2>&1 || { tail -30 $O/pytest_early.log; exit 1; }
+tail -1 $O/pytest_early.log
+timeout -k 10 300 python scripts/rank_balance.py --workload c4_bunny4k --ranks 2,4,8 --stripe-rows 8 > $O/rank_balance_c4.jsonl 2> $O/rank_balance_c4.err || { tail -20 $O/rank_balance_c4.err; exit 1; }
+python3 -c "
+import json
+for l in open('$O/rank_balance_c4.jsonl'):
+    d=json.loads(l); print(d['workload'], d['stripe_rows'], d['n'], 'imb time %.4f seg %.4f pred %.0f one-gpu %.0f' % (d['imbalance_time'], d['imbalance_segments'], d['predicted_value_Mrays'], d['one_gpu_equiv_Mrays']))"
 echo done
