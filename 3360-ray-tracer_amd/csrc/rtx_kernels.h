@@ -31,7 +31,11 @@ constexpr int kParkAt = 16;  // PARK kernel: park traversals once at most this m
 // kChunk): the plain kernel 256 (ab_chunk_*; 512 C2 -0.4 %), the PARK kernel 512 (bunny C3
 // +0.7 %, profiles/r04/ab_chunk_map0_r6e_*.txt)
 constexpr int kChunkPlain = 256, kChunkPark = 512;
-constexpr int kChunkShared = 128;  // the same for the block-shared chunks (adaptive phase launches)
+// the same for the block-shared chunks of the adaptive phase launches (MAP 1; <= 511: ChunkLds),
+// by schedule: the PARK kernel 128 (64: -0.3 %, 256: -2.1 % C3 adaptive), the plain kernel 256
+// (C2 adaptive +1.0 % over 128; 64: -3.6 %) (profiles/r06/ab/ab_r10c_c3a.txt, ab_r10c_c2a.txt)
+constexpr int kChunkSharedPlain = 256, kChunkSharedPark = 128;
+static_assert(kChunkSharedPlain <= 511 && kChunkSharedPark <= 511, "ChunkLds keeps a chunk's size in 9 bits");
 
 // Pixel subset of the image handled by one call (rectangle or interleaved row stripes).
 struct PixelMap {
@@ -146,9 +150,12 @@ struct PixelSoA {
 constexpr bool spec_walk(int park, bool fast, bool scatter) { return park == 2 && fast && !scatter; }
 constexpr int64_t kSpecMaxNodes = 65536;
 // The slot chunks of an adaptive phase launch (MAP == 1), one word per wave of the block: a
-// chunk of kChunk slots of one slot region, claimed by LDS adds to its cursor, by its wave and,
-// once the slot counters are dry, by the other waves of the block too.
-// word = region (3 bits) | chunk index in the region (29 bits) | cursor (32 bits)
+// chunk of up to kChunkShared slots of one slot region, claimed by LDS adds to its cursor, by its
+// wave and, once the slot counters are dry, by the other waves of the block too.
+// word = first slot (32 bits) | slots in the chunk (9 bits) | cursor (23 bits): a claim decodes
+// its slots from the word alone (32-bit arithmetic; the region bounds are needed only to install
+// a chunk).  The cursor cannot reach bit 23: a wave adds at most 64 per claim, and the claims on a
+// word between two installs are bounded by the block's four chunks (at most ~6 k adds).
 struct ChunkLds {
   unsigned long long w[kBlock / 64];
 };
@@ -280,6 +287,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   // an implicit instantiation anywhere else is a compile error, not a silently different kernel
   static_assert((PARK > 0) == (RTX_PARK_TU != 0), "k_persistent: PARK kernels belong to rtx_park.hip");
   constexpr int kChunk = PARK ? kChunkPark : kChunkPlain;
+  constexpr int kChunkShared = PARK ? kChunkSharedPark : kChunkSharedPlain;
   const PersistLds lay = persist_lds(A.stack_slots, kSpecLds, block_region_kind(MAP, SCATTER));
   char* const ldsb = (char*)lds;
   // counting builds: the launch's timeline (wall clock, 100 MHz): [13] ~first block start,
@@ -289,7 +297,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   unsigned long long* const cw = (unsigned long long*)(ldsb + lay.block);  // (kShared) the chunk words
   (void)cw;
   if (kShared) {
-    if (threadIdx.x < kBlock / 64) cw[threadIdx.x] = (unsigned long long)kChunkShared;  // (no chunk: cursor past any)
+    if (threadIdx.x < kBlock / 64) cw[threadIdx.x] = 0ull;  // (no chunk: zero slots)
     __syncthreads();
   }
   uint32_t* stk = (uint32_t*)(ldsb + lay.stack) + threadIdx.x;
@@ -350,12 +358,9 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
           unsigned long long old = 0;
           if (lane_id() == 0) old = atomicAdd(&cw[j], (unsigned long long)(nidle - given));
           old = __shfl(old, 0);
-          const uint32_t r = (uint32_t)(old >> 61), id = (uint32_t)(old >> 32) & 0x1FFFFFFFu, cur = (uint32_t)old;
-          const uint64_t rs = ((uint64_t)r * nslots) >> 3, re = ((uint64_t)(r + 1) * nslots) >> 3;
-          const uint64_t cs = rs + (uint64_t)id * kChunkShared;
-          const uint32_t csz = cs < re ? (uint32_t)min<uint64_t>(kChunkShared, re - cs) : 0u;
+          const uint32_t cs = (uint32_t)(old >> 32), csz = ((uint32_t)old >> 23) & 0x1FFu, cur = (uint32_t)old & 0x7FFFFFu;
           const uint32_t got = cur < csz ? min(nidle - given, csz - cur) : 0u;
-          if (!has && rank >= given && rank < given + got) slot = (uint32_t)(cs + cur + (rank - given)), fresh = true;
+          if (!has && rank >= given && rank < given + got) slot = cs + cur + (rank - given), fresh = true;
           given += got;
         };
         take(wv);
@@ -368,8 +373,8 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
             const uint64_t rs = ((uint64_t)region * nslots) >> 3, re = ((uint64_t)(region + 1) * nslots) >> 3;
             if (rs + b < re) {
               ok = true;
-              if (lane_id() == 0)
-                atomicExch(&cw[wv], ((unsigned long long)((region << 29) | (uint32_t)(b / kChunkShared)) << 32));
+              const uint32_t csz = (uint32_t)min<uint64_t>(kChunkShared, re - (rs + b));
+              if (lane_id() == 0) atomicExch(&cw[wv], ((unsigned long long)(rs + b) << 32) | ((unsigned long long)csz << 23));
             } else {
               region = (region + 1) & 7;
             }
@@ -435,7 +440,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
       // scratch 80 -> 16 B; the bunny's Lambertian texture-free builds lost 1.0 % (their spilled
       // SGPRs 79 -> 60, scratch 52 -> 0 B), so they keep the arguments in registers;
       // profiles/r03/ab_kernarg_refill_r4g_*).
-      constexpr bool kArgsAtRefill = !(LAMB && NOTEX);
+      constexpr bool kArgsAtRefill = !(LAMB && NOTEX);  // (also for the MAP 1 builds: -0.3 %, r10b)
       auto kseg = __builtin_amdgcn_kernarg_segment_ptr();
       if (kArgsAtRefill) asm volatile("" : "+s"(kseg));
       const RenderArgs& Ar = kArgsAtRefill ? *(const RenderArgs*)kseg : A;
