@@ -1547,8 +1547,8 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     if ((rc = sink->copy(sink->ctx, 0, npix, s))) return rc;
   }
   if (timed) {  // the statistics come back with the frame: one wait, no blocking copy after it
-    if ((rc = sc->counters_h.reserve(18 * sizeof(unsigned long long)))) return rc;
-    HIPC(hipMemcpyAsync(sc->counters_h.p, cnt, 18 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    if ((rc = sc->counters_h.reserve(24 * sizeof(unsigned long long)))) return rc;
+    HIPC(hipMemcpyAsync(sc->counters_h.p, cnt, 24 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     HIPC(hipEventRecord(sc->ev[4], s));
   }
   if (banded) {  // the caller's stream owns the output again once the band copies are done
@@ -1568,9 +1568,18 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
       HIPC(hipEventElapsedTime(&hms, sc->evpool[e], sc->evpool[e + 1]));
       hot_ms += hms;
     }
-    unsigned long long h[18];
+    unsigned long long h[24];
     std::memcpy(h, sc->counters_h.p, sizeof h);
     static const bool drain_debug = std::getenv("RTX_DEBUG_DRAIN") != nullptr;
+    static const bool region_debug = std::getenv("RTX_DEBUG_REGIONS") != nullptr;
+    if (region_debug && (h[18] | h[19] | h[20])) {  // counting builds: the persistent loop's regions
+      const double tot = (double)(h[18] + h[19] + h[20]);
+      fprintf(stderr,
+              "rtx regions: wave cycles refill %.4f walk %.4f shade %.4f of %.4g; shading rounds %llu, lanes per "
+              "shading round %.2f; segments %llu\n",
+              h[18] / tot, h[19] / tot, h[20] / tot, tot, (unsigned long long)h[21], h[21] ? (double)h[22] / h[21] : 0.0,
+              (unsigned long long)h[0]);
+    }
     if (drain_debug && h[13] && !phased) {  // counting builds: the (last) launch's timeline
       const double t0 = (double)~h[13];
       auto us = [&](unsigned long long v) { return ((double)v - t0) / 100.0; };

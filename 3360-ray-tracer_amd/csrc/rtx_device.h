@@ -597,6 +597,12 @@ struct Counters {
   uint32_t tris, sphs;      // primitive tests by kind (rects = prims - tris - sphs)
   uint32_t witers, widle;   // persistent kernel: wave loop rounds, and those with no path to trace
   uint32_t wlive;           // ... and the lanes with a path, summed over the rounds that trace
+  // persistent kernel, counting builds: the wave's shader-clock cycles (s_memtime) in the loop's
+  // regions — refill (ballot, slot claim, primary ray), walk (closest hit, parked walks
+  // included), shading (hit record, BSDF, Russian roulette, radiance store) — and the lanes that
+  // shaded, summed over the rounds (counted by the first active lane, wave-uniform)
+  uint64_t cyc_refill, cyc_walk, cyc_shade;
+  uint32_t wshade, lshade;
 };
 __device__ __forceinline__ void count_prim(Counters& c, const rtx_prim* P) {
   c.prims++;

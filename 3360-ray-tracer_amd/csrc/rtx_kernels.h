@@ -197,6 +197,11 @@ __device__ __forceinline__ void flush_counters(const RenderArgs& A, const Counte
     if (c.witers) atomicAdd(&A.counters[10], (unsigned long long)c.witers);
     if (c.widle) atomicAdd(&A.counters[11], (unsigned long long)c.widle);
     if (c.wlive) atomicAdd(&A.counters[12], (unsigned long long)c.wlive);
+    if (c.cyc_refill) atomicAdd(&A.counters[18], c.cyc_refill);
+    if (c.cyc_walk) atomicAdd(&A.counters[19], c.cyc_walk);
+    if (c.cyc_shade) atomicAdd(&A.counters[20], c.cyc_shade);
+    if (c.wshade) atomicAdd(&A.counters[21], (unsigned long long)c.wshade);
+    if (c.lshade) atomicAdd(&A.counters[22], (unsigned long long)c.lshade);
   }
   if (segs) atomicAdd(&A.counters[0], (unsigned long long)segs);
   if (prims) atomicAdd(&A.counters[1], (unsigned long long)prims);
@@ -337,7 +342,22 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   const bool park_ok = kPark && A.S.use_bvh && !A.S.froot_leaf;
   bool parked = false;
   TravState trs;
+  // counting builds: region timestamps (s_memtime, wave-uniform); t_walk is set by the lanes
+  // that traced this round and read at the next loop top, where the wave has reconverged
+  uint64_t t_top = 0, t_seg = 0, t_walk = 0;
+  (void)t_top, (void)t_seg, (void)t_walk;
   while (true) {
+    if (COUNT) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      const unsigned long long tw = __ballot(t_walk != 0);
+      if (t_seg && tw) {  // the previous round traced: refill .. walk .. shading
+        const uint64_t w = __shfl(t_walk, __ffsll((long long)tw) - 1);
+        if (lane_id() == 0) c.cyc_refill += t_seg - t_top, c.cyc_walk += w - t_seg, c.cyc_shade += now - w;
+      } else if (t_top && lane_id() == 0) {
+        c.cyc_refill += now - t_top;  // (a round with nothing to trace: all refill / waiting)
+      }
+      t_top = now, t_seg = 0, t_walk = 0;
+    }
     // ---- refill: ballot of idle lanes, leftover of the current chunk first.  Refilling
     // only once kRefillMin lanes are idle (or the wave is empty) amortises the
     // primary-generation code over several lanes.
@@ -480,6 +500,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
       const uint32_t live = (uint32_t)__popcll(__ballot(has));
       if (lane_id() == 0) c.wlive += live;
     }
+    if (COUNT) t_seg = __builtin_amdgcn_s_memtime();
     if (!has) continue;
     // ---- one segment: closest hit + shading ----
     V3 L;
@@ -504,6 +525,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
                      : trace4_run<STACK, COUNT, TK>(A.S, P.o, P.d, tmin, stk, kBlock, c, trs,
                                                     active > kParkAt ? kParkAt : -1);
         parked = !done;
+        if (COUNT) t_walk = __builtin_amdgcn_s_memtime();
         if (parked) continue;
         best = trs.best, tb = trs.closest, bmat = trs.mat;
       } else if (kPark) {  // no BVH, or its root is a leaf
@@ -512,7 +534,12 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
         best = trace<STACK, FAST, COUNT, TK>(A.S, P.o, P.d, tmin, kInf, stk, c, tb, bmat);
       }
       segs++;
-      if (COUNT) pseg++;
+      if (COUNT) {
+        pseg++;
+        if (!kPark || !park_ok) t_walk = __builtin_amdgcn_s_memtime();
+        const unsigned long long sh = __ballot(1);
+        if ((int)lane_id() == __ffsll((long long)sh) - 1) c.wshade++, c.lshade += (uint32_t)__popcll(sh);
+      }
       Hit h;
       rtx_material m;
       if (best >= 0) finish_hit_at<false>(A.S, best, tb, P.o, P.d, h);
