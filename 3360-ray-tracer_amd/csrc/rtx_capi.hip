@@ -1575,10 +1575,10 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     if (region_debug && (h[18] | h[19] | h[20])) {  // counting builds: the persistent loop's regions
       const double tot = (double)(h[18] + h[19] + h[20]);
       fprintf(stderr,
-              "rtx regions: wave cycles refill %.4f walk %.4f shade %.4f of %.4g; shading rounds %llu, lanes per "
-              "shading round %.2f; segments %llu\n",
-              h[18] / tot, h[19] / tot, h[20] / tot, tot, (unsigned long long)h[21], h[21] ? (double)h[22] / h[21] : 0.0,
-              (unsigned long long)h[0]);
+              "rtx regions: wave cycles refill %.4f walk %.4f shade %.4f of %.4g (leaf rounds of the speculative "
+              "walk %.4f); shading rounds %llu, lanes per shading round %.2f; segments %llu\n",
+              h[18] / tot, h[19] / tot, h[20] / tot, tot, h[23] / tot, (unsigned long long)h[21],
+              h[21] ? (double)h[22] / h[21] : 0.0, (unsigned long long)h[0]);
     }
     if (drain_debug && h[13] && !phased) {  // counting builds: the (last) launch's timeline
       const double t0 = (double)~h[13];

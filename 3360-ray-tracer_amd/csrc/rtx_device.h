@@ -603,6 +603,7 @@ struct Counters {
   // shaded, summed over the rounds (counted by the first active lane, wave-uniform)
   uint64_t cyc_refill, cyc_walk, cyc_shade;
   uint32_t wshade, lshade;
+  uint64_t cyc_leaf;  // ... of which the speculative walk's leaf rounds (trace4_run_spec)
 };
 __device__ __forceinline__ void count_prim(Counters& c, const rtx_prim* P) {
   c.prims++;
@@ -994,6 +995,8 @@ __device__ __forceinline__ bool trace4_run_spec(const DScene& S, V3 o, V3 d, dou
     }
     const bool can_visit = walking && !park && qn <= F - 4;
     if (__ballot(can_visit) == 0 || __popcll(__ballot(qn != 0)) >= kLeafSpecMin) {
+      uint64_t tl0 = 0;
+      if (COUNT) tl0 = __builtin_amdgcn_s_memtime();
       if (qn != 0) {  // one queued leaf, in visit order
         const uint32_t cur = lq[qh * stride];
         qh = (qh + 1) & (F - 1), qn--;
@@ -1007,6 +1010,7 @@ __device__ __forceinline__ bool trace4_run_spec(const DScene& S, V3 o, V3 d, dou
           tmax_x = tmax_f * 1.00001f;
         }
       }
+      if (COUNT && first_active_lane()) cnt.cyc_leaf += __builtin_amdgcn_s_memtime() - tl0;
     }
     if (!walking && qn == 0) break;
   }

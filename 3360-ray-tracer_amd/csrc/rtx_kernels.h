@@ -202,6 +202,7 @@ __device__ __forceinline__ void flush_counters(const RenderArgs& A, const Counte
     if (c.cyc_shade) atomicAdd(&A.counters[20], c.cyc_shade);
     if (c.wshade) atomicAdd(&A.counters[21], (unsigned long long)c.wshade);
     if (c.lshade) atomicAdd(&A.counters[22], (unsigned long long)c.lshade);
+    if (c.cyc_leaf) atomicAdd(&A.counters[23], c.cyc_leaf);
   }
   if (segs) atomicAdd(&A.counters[0], (unsigned long long)segs);
   if (prims) atomicAdd(&A.counters[1], (unsigned long long)prims);
