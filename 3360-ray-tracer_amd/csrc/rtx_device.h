@@ -10,6 +10,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "rtx.h"
 
 // Per-translation-unit choices.  rtx_park.hip, which compiles the PARK instantiations of
@@ -597,13 +599,17 @@ struct Counters {
   uint32_t tris, sphs;      // primitive tests by kind (rects = prims - tris - sphs)
   uint32_t witers, widle;   // persistent kernel: wave loop rounds, and those with no path to trace
   uint32_t wlive;           // ... and the lanes with a path, summed over the rounds that trace
-  // persistent kernel, counting builds: the wave's shader-clock cycles (s_memtime) in the loop's
-  // regions — refill (ballot, slot claim, primary ray), walk (closest hit, parked walks
-  // included), shading (hit record, BSDF, Russian roulette, radiance store) — and the lanes that
-  // shaded, summed over the rounds (counted by the first active lane, wave-uniform)
-  uint64_t cyc_refill, cyc_walk, cyc_shade;
+};
+// Persistent kernel, counting builds only (k_persistent's counter type is CountersClk when COUNT,
+// plain Counters otherwise, so the product builds' code is untouched by this): the wave's
+// shader-clock cycles (s_memtime) in the loop's regions — refill (ballot, slot claim, primary
+// ray), walk (closest hit, parked walks included; of which the speculative walk's leaf rounds),
+// shading (hit record, BSDF, Russian roulette, radiance store) — and the lanes that shaded,
+// summed over the rounds (wave-uniform: counted by lane 0 or the first active lane).
+struct CountersClk : Counters {
+  uint64_t t_top, t_seg, t_walk, t_leaf;  // the current round's stamps (t_walk: set by the lanes that traced)
+  uint64_t cyc_refill, cyc_walk, cyc_shade, cyc_leaf;
   uint32_t wshade, lshade;
-  uint64_t cyc_leaf;  // ... of which the speculative walk's leaf rounds (trace4_run_spec)
 };
 __device__ __forceinline__ void count_prim(Counters& c, const rtx_prim* P) {
   c.prims++;
@@ -956,9 +962,9 @@ constexpr int kLeafSpecMin = 8;
 // tie order are unchanged.  A lane parks only with an empty queue, between visits.  The stack
 // holds 16-bit node indices (the host runs this kernel only on trees under 2^16 nodes), so
 // stack and queue fit the LDS of four blocks per CU.
-template <int STACK, bool COUNT, int KIND = -1>
+template <int STACK, bool COUNT, int KIND = -1, class CNT = Counters>
 __device__ __forceinline__ bool trace4_run_spec(const DScene& S, V3 o, V3 d, double tmin, uint16_t* stk,
-                                                uint32_t* lq, int stride, Counters& cnt, TravState& ts,
+                                                uint32_t* lq, int stride, CNT& cnt, TravState& ts,
                                                 int park_at) {
   constexpr uint32_t F = kLeafQueue;
   static_assert(F >= 8 && (F & (F - 1)) == 0, "leaf queue: a power of two >= 8");
@@ -995,8 +1001,7 @@ __device__ __forceinline__ bool trace4_run_spec(const DScene& S, V3 o, V3 d, dou
     }
     const bool can_visit = walking && !park && qn <= F - 4;
     if (__ballot(can_visit) == 0 || __popcll(__ballot(qn != 0)) >= kLeafSpecMin) {
-      uint64_t tl0 = 0;
-      if (COUNT) tl0 = __builtin_amdgcn_s_memtime();
+      if constexpr (std::is_same_v<CNT, CountersClk>) cnt.t_leaf = __builtin_amdgcn_s_memtime();
       if (qn != 0) {  // one queued leaf, in visit order
         const uint32_t cur = lq[qh * stride];
         qh = (qh + 1) & (F - 1), qn--;
@@ -1010,7 +1015,8 @@ __device__ __forceinline__ bool trace4_run_spec(const DScene& S, V3 o, V3 d, dou
           tmax_x = tmax_f * 1.00001f;
         }
       }
-      if (COUNT && first_active_lane()) cnt.cyc_leaf += __builtin_amdgcn_s_memtime() - tl0;
+      if constexpr (std::is_same_v<CNT, CountersClk>)
+        if (first_active_lane()) cnt.cyc_leaf += __builtin_amdgcn_s_memtime() - cnt.t_leaf;
     }
     if (!walking && qn == 0) break;
   }

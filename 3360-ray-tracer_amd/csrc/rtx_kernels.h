@@ -185,6 +185,15 @@ __device__ __forceinline__ int64_t trace(const DScene& S, V3 o, V3 d, double tmi
   return trace<STACK, FAST, COUNT>(S, o, d, tmin, tmax, stk, c, t_best, m);
 }
 
+// counting builds of the persistent kernel: the loop's region cycles (CountersClk)
+__device__ __forceinline__ void flush_clock(const RenderArgs& A, const CountersClk& c) {
+  if (c.cyc_refill) atomicAdd(&A.counters[18], c.cyc_refill);
+  if (c.cyc_walk) atomicAdd(&A.counters[19], c.cyc_walk);
+  if (c.cyc_shade) atomicAdd(&A.counters[20], c.cyc_shade);
+  if (c.wshade) atomicAdd(&A.counters[21], (unsigned long long)c.wshade);
+  if (c.lshade) atomicAdd(&A.counters[22], (unsigned long long)c.lshade);
+  if (c.cyc_leaf) atomicAdd(&A.counters[23], c.cyc_leaf);
+}
 __device__ __forceinline__ void flush_counters(const RenderArgs& A, const Counters& c, uint32_t segs,
                                                uint32_t prims, bool count) {
   if (count) {
@@ -197,12 +206,6 @@ __device__ __forceinline__ void flush_counters(const RenderArgs& A, const Counte
     if (c.witers) atomicAdd(&A.counters[10], (unsigned long long)c.witers);
     if (c.widle) atomicAdd(&A.counters[11], (unsigned long long)c.widle);
     if (c.wlive) atomicAdd(&A.counters[12], (unsigned long long)c.wlive);
-    if (c.cyc_refill) atomicAdd(&A.counters[18], c.cyc_refill);
-    if (c.cyc_walk) atomicAdd(&A.counters[19], c.cyc_walk);
-    if (c.cyc_shade) atomicAdd(&A.counters[20], c.cyc_shade);
-    if (c.wshade) atomicAdd(&A.counters[21], (unsigned long long)c.wshade);
-    if (c.lshade) atomicAdd(&A.counters[22], (unsigned long long)c.lshade);
-    if (c.cyc_leaf) atomicAdd(&A.counters[23], c.cyc_leaf);
   }
   if (segs) atomicAdd(&A.counters[0], (unsigned long long)segs);
   if (prims) atomicAdd(&A.counters[1], (unsigned long long)prims);
@@ -319,7 +322,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   const uint64_t nslots = MAP == 1 ? (uint64_t)next_slot[8 * 16] : (uint64_t)A.npix * (uint64_t)A.K;
   // GetPixel uses Interval(0.001, inf) (camera.h:158); IntersectBatch uses 0.001f (cpu_ray_integrator.h:21)
   const double tmin = SCATTER ? 0.001 : (double)0.001f;
-  Counters c{};
+  std::conditional_t<COUNT, CountersClk, Counters> c{};
   uint32_t segs = 0, prims = 0;
   // counting builds: the lane's path segments, stored per slot when the launch's slot counter
   // block names a buffer for them (adaptive renders: the segments of the recorded samples)
@@ -343,21 +346,19 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
   const bool park_ok = kPark && A.S.use_bvh && !A.S.froot_leaf;
   bool parked = false;
   TravState trs;
-  // counting builds: region timestamps (s_memtime, wave-uniform); t_walk is set by the lanes
-  // that traced this round and read at the next loop top, where the wave has reconverged
-  uint64_t t_top = 0, t_seg = 0, t_walk = 0;
-  (void)t_top, (void)t_seg, (void)t_walk;
   while (true) {
-    if (COUNT) {
+    // counting builds: region stamps (s_memtime, wave-uniform); t_walk is set by the lanes that
+    // traced this round and read here, at the next loop top, where the wave has reconverged
+    if constexpr (COUNT) {
       const uint64_t now = __builtin_amdgcn_s_memtime();
-      const unsigned long long tw = __ballot(t_walk != 0);
-      if (t_seg && tw) {  // the previous round traced: refill .. walk .. shading
-        const uint64_t w = __shfl(t_walk, __ffsll((long long)tw) - 1);
-        if (lane_id() == 0) c.cyc_refill += t_seg - t_top, c.cyc_walk += w - t_seg, c.cyc_shade += now - w;
-      } else if (t_top && lane_id() == 0) {
-        c.cyc_refill += now - t_top;  // (a round with nothing to trace: all refill / waiting)
+      const unsigned long long tw = __ballot(c.t_walk != 0);
+      if (c.t_seg && tw) {  // the previous round traced: refill .. walk .. shading
+        const uint64_t w = __shfl(c.t_walk, __ffsll((long long)tw) - 1);
+        if (lane_id() == 0) c.cyc_refill += c.t_seg - c.t_top, c.cyc_walk += w - c.t_seg, c.cyc_shade += now - w;
+      } else if (c.t_top && lane_id() == 0) {
+        c.cyc_refill += now - c.t_top;  // (a round with nothing to trace: all refill / waiting)
       }
-      t_top = now, t_seg = 0, t_walk = 0;
+      c.t_top = now, c.t_seg = 0, c.t_walk = 0;
     }
     // ---- refill: ballot of idle lanes, leftover of the current chunk first.  Refilling
     // only once kRefillMin lanes are idle (or the wave is empty) amortises the
@@ -501,7 +502,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
       const uint32_t live = (uint32_t)__popcll(__ballot(has));
       if (lane_id() == 0) c.wlive += live;
     }
-    if (COUNT) t_seg = __builtin_amdgcn_s_memtime();
+    if constexpr (COUNT) c.t_seg = __builtin_amdgcn_s_memtime();
     if (!has) continue;
     // ---- one segment: closest hit + shading ----
     V3 L;
@@ -526,7 +527,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
                      : trace4_run<STACK, COUNT, TK>(A.S, P.o, P.d, tmin, stk, kBlock, c, trs,
                                                     active > kParkAt ? kParkAt : -1);
         parked = !done;
-        if (COUNT) t_walk = __builtin_amdgcn_s_memtime();
+        if constexpr (COUNT) c.t_walk = __builtin_amdgcn_s_memtime();
         if (parked) continue;
         best = trs.best, tb = trs.closest, bmat = trs.mat;
       } else if (kPark) {  // no BVH, or its root is a leaf
@@ -535,9 +536,9 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
         best = trace<STACK, FAST, COUNT, TK>(A.S, P.o, P.d, tmin, kInf, stk, c, tb, bmat);
       }
       segs++;
-      if (COUNT) {
+      if constexpr (COUNT) {
         pseg++;
-        if (!kPark || !park_ok) t_walk = __builtin_amdgcn_s_memtime();
+        if (!kPark || !park_ok) c.t_walk = __builtin_amdgcn_s_memtime();
         const unsigned long long sh = __ballot(1);
         if ((int)lane_id() == __ffsll((long long)sh) - 1) c.wshade++, c.lshade += (uint32_t)__popcll(sh);
       }
@@ -590,6 +591,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
     }
   }
   flush_counters(A, c, segs, prims, COUNT);
+  if constexpr (COUNT) flush_clock(A, c);
   if (COUNT && lane_id() == 0) {
     const unsigned long long t = (unsigned long long)wall_clock64();
     atomicMax(&A.counters[16], t);
