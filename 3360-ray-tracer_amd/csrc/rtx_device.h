@@ -962,7 +962,7 @@ constexpr int kLeafSpecMin = 8;
 // tie order are unchanged.  A lane parks only with an empty queue, between visits.  The stack
 // holds 16-bit node indices (the host runs this kernel only on trees under 2^16 nodes), so
 // stack and queue fit the LDS of four blocks per CU.
-template <int STACK, bool COUNT, int KIND = -1, class CNT = Counters>
+template <int STACK, bool COUNT, int KIND = -1, class CNT = Counters, int LEAFMIN = kLeafSpecMin>
 __device__ __forceinline__ bool trace4_run_spec(const DScene& S, V3 o, V3 d, double tmin, uint16_t* stk,
                                                 uint32_t* lq, int stride, CNT& cnt, TravState& ts,
                                                 int park_at) {
@@ -1000,7 +1000,7 @@ __device__ __forceinline__ bool trace4_run_spec(const DScene& S, V3 o, V3 d, dou
       walking = visit_next<STACK, uint16_t>(tt, cc, false, closest, tmax_f, tmax_x, stk, stride, sp, node);
     }
     const bool can_visit = walking && !park && qn <= F - 4;
-    if (__ballot(can_visit) == 0 || __popcll(__ballot(qn != 0)) >= kLeafSpecMin) {
+    if (__ballot(can_visit) == 0 || __popcll(__ballot(qn != 0)) >= LEAFMIN) {
       if constexpr (std::is_same_v<CNT, CountersClk>) cnt.t_leaf = __builtin_amdgcn_s_memtime();
       if (qn != 0) {  // one queued leaf, in visit order
         const uint32_t cur = lq[qh * stride];

@@ -521,11 +521,20 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
           trav_globals<COUNT>(A.S, P.o, P.d, tmin, c, trs);
         }
         // parking only when some lane of this round finishes first: every round makes progress
+#ifndef RTX_AB_LEAFMIN_MAP1
+#define RTX_AB_LEAFMIN_MAP1 kLeafSpecMin
+#endif
+#ifndef RTX_AB_PARKAT_MAP1
+#define RTX_AB_PARKAT_MAP1 kParkAt
+#endif
+        constexpr int kLeafMinK = MAP == 1 ? RTX_AB_LEAFMIN_MAP1 : kLeafSpecMin;
+        constexpr int kParkAtK = MAP == 1 ? RTX_AB_PARKAT_MAP1 : kParkAt;
         const bool done =
-            kSpecLds ? trace4_run_spec<STACK, COUNT, TK>(A.S, P.o, P.d, tmin, stk16, leafq, kBlock, c, trs,
-                                                         active > kParkAt ? kParkAt : -1)
+            kSpecLds ? trace4_run_spec<STACK, COUNT, TK, decltype(c), kLeafMinK>(A.S, P.o, P.d, tmin, stk16, leafq,
+                                                                                kBlock, c, trs,
+                                                                                active > kParkAtK ? kParkAtK : -1)
                      : trace4_run<STACK, COUNT, TK>(A.S, P.o, P.d, tmin, stk, kBlock, c, trs,
-                                                    active > kParkAt ? kParkAt : -1);
+                                                    active > kParkAtK ? kParkAtK : -1);
         parked = !done;
         if constexpr (COUNT) c.t_walk = __builtin_amdgcn_s_memtime();
         if (parked) continue;
