@@ -603,6 +603,7 @@ int64_t subset_pixels(const rtx_camera* cam, const rtx_render_params* p, PixelMa
     for (int y = 0; y < m.H; y++)
       if ((y / m.srows) % m.scount == m.sidx) rows++;
     m.x0 = m.y0 = 0, m.w = m.W, m.h = (int)rows;
+    set_map_div(m);
     return rows * (int64_t)m.W;
   }
   m.stripes = 0;
@@ -613,6 +614,7 @@ int64_t subset_pixels(const rtx_camera* cam, const rtx_render_params* p, PixelMa
     return -1;
   }
   m.srows = 1, m.sidx = 0, m.scount = 1;
+  set_map_div(m);
   return (int64_t)m.w * m.h;
 }
 
@@ -896,7 +898,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   RenderArgs A1 = A;
   A1.L = sc->lbuf.as<double>();
   A1.conv = nullptr;
-  A1.K = K1, A1.s0 = 0;
+  A1.K = K1, A1.s0 = 0, A1.fK = make_fastdiv((uint32_t)K1);
   // the phase kernel without a slot map (uniform groups: slot p * K1 + k), for its block-shared
   // chunks: the first pass ends as the phases do, its last slots traced by whole blocks
   Launch L1 = L;
@@ -908,7 +910,7 @@ int render_adaptive(rtx_scene* sc, const Launch& L, const RenderArgs& A, const r
   RenderArgs Ag = A;
   Ag.L = w.lbuf.as<double>();
   Ag.conv = nullptr;    // only pixels still sampling have slots
-  Ag.K = 1, Ag.s0 = 0;  // (unused: slots from the phase's slot map)
+  Ag.K = 1, Ag.s0 = 0, Ag.fK = make_fastdiv(1u);  // (unused: slots from the phase's slot map)
   Launch Lg = L;
   Lg.map = 1;
   for (int g = 2;; g++) {
@@ -1467,6 +1469,7 @@ static int render_device_impl(rtx_scene* sc, const rtx_camera* cam, const rtx_re
     if (prm->adaptive && prm->samples_per_group <= 0)
       Kc = std::min(Kc, s0 < prm->min_spp ? prm->min_spp - s0 : 4);
     A.K = Kc;
+    A.fK = make_fastdiv((uint32_t)Kc);
     A.s0 = s0;
     auto hot_begin = [&]() -> int {
       if (timed) {
@@ -1951,6 +1954,16 @@ extern "C" int rtx_internal_adapt_tune(int64_t phase_slots, int32_t phase_kcap, 
                                        double margin1, double pool_w) {
   if (phase_slots < 0 || phase_kcap < 0 || first_map > 1) return fail(RTX_ERR_INVALID, "bad tuning value");
   g_tune = AdaptTune{phase_slots, phase_kcap, first_map, phase_mstep, margin1, pool_w};
+  return RTX_OK;
+}
+
+// Test hook (not in rtx.h): the launch-constant division of the kernels (FastDiv, the slot ->
+// pixel and pixel -> row maps) on the host: out[i] = n[i] / d for i < cnt.
+extern "C" int rtx_internal_fastdiv(uint32_t d, const uint32_t* n, int64_t cnt, uint32_t* out) {
+  if ((!n || !out) && cnt > 0) return fail(RTX_ERR_INVALID, "NULL argument");
+  if (d == 0) return fail(RTX_ERR_INVALID, "division by zero");
+  const FastDiv f = make_fastdiv(d);
+  for (int64_t i = 0; i < cnt; i++) out[i] = f.div(n[i]);
   return RTX_OK;
 }
 

@@ -207,8 +207,9 @@ __device__ __forceinline__ void sincos_small(double x, double& sn, double& cs) {
   cs = quad > 1 ? -c0 : c0;
   sn = quad > 1 ? -s0 : s0;
 }
+template <bool SMALL = kSincosSmall>
 __device__ __forceinline__ void cos_sin(double phi, double& c, double& s) {
-  if constexpr (kSincosSmall) {
+  if constexpr (SMALL) {
     double t;
     sincos_small(phi, t, c);
     asm volatile("" : "+v"(c));
@@ -962,7 +963,7 @@ constexpr int kLeafSpecMin = 8;
 // tie order are unchanged.  A lane parks only with an empty queue, between visits.  The stack
 // holds 16-bit node indices (the host runs this kernel only on trees under 2^16 nodes), so
 // stack and queue fit the LDS of four blocks per CU.
-template <int STACK, bool COUNT, int KIND = -1, class CNT = Counters, int LEAFMIN = kLeafSpecMin>
+template <int STACK, bool COUNT, int KIND = -1, class CNT = Counters>
 __device__ __forceinline__ bool trace4_run_spec(const DScene& S, V3 o, V3 d, double tmin, uint16_t* stk,
                                                 uint32_t* lq, int stride, CNT& cnt, TravState& ts,
                                                 int park_at) {
@@ -1000,7 +1001,7 @@ __device__ __forceinline__ bool trace4_run_spec(const DScene& S, V3 o, V3 d, dou
       walking = visit_next<STACK, uint16_t>(tt, cc, false, closest, tmax_f, tmax_x, stk, stride, sp, node);
     }
     const bool can_visit = walking && !park && qn <= F - 4;
-    if (__ballot(can_visit) == 0 || __popcll(__ballot(qn != 0)) >= LEAFMIN) {
+    if (__ballot(can_visit) == 0 || __popcll(__ballot(qn != 0)) >= kLeafSpecMin) {
       if constexpr (std::is_same_v<CNT, CountersClk>) cnt.t_leaf = __builtin_amdgcn_s_memtime();
       if (qn != 0) {  // one queued leaf, in visit order
         const uint32_t cur = lq[qh * stride];
@@ -1391,7 +1392,7 @@ __device__ __forceinline__ void shade_core(const DScene& S, int max_depth, Path&
   if (isL) {
     const double phi = 2.0 * kPi * r1;
     double cph, sph;
-    cos_sin(phi, cph, sph);
+    cos_sin<kSincosSmall || !LAMB>(phi, cph, sph);
     x = s2 * cph;
     y = s2 * sph;
   }

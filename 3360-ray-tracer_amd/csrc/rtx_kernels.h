@@ -37,26 +37,55 @@ constexpr int kChunkPlain = 256, kChunkPark = 512;
 constexpr int kChunkSharedPlain = 256, kChunkSharedPark = 128;
 static_assert(kChunkSharedPlain <= 511 && kChunkSharedPark <= 511, "ChunkLds keeps a chunk's size in 9 bits");
 
+// Unsigned 32-bit division by a divisor fixed for a launch: one multiply-high, a subtract and
+// two shifts (Granlund & Montgomery 1994; Hacker's Delight §10-9) instead of the ~17
+// instructions of a runtime division (a float reciprocal, its corrections and three 32-bit
+// multiplies, which do not pair).  For d >= 2, l = ceil(log2 d), m = floor(2^32 (2^l - d) / d) + 1
+// and q = (t + ((n - t) >> 1)) >> (l - 1) with t = mulhi(n, m), exact for every n < 2^32;
+// d = 1: m = 0 and no shifts.  tests/test_capi_exports.py checks it against the division.
+struct FastDiv {
+  uint32_t m, sh;  // magic; shifts: sh & 0xFF first (0 or 1), sh >> 8 second (l - 1)
+  __host__ __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    const uint32_t t = (uint32_t)(((uint64_t)n * m) >> 32);
+    return (t + ((n - t) >> (sh & 0xFFu))) >> (sh >> 8);
+  }
+};
+inline FastDiv make_fastdiv(uint32_t d) {  // host side; d >= 1
+  if (d <= 1) return FastDiv{0u, 0u};
+  uint32_t l = 0;
+  while (l < 32 && (1ull << l) < d) l++;
+  const uint64_t m = ((((uint64_t)1 << 32) * (((uint64_t)1 << l) - d)) / d) + 1;
+  return FastDiv{(uint32_t)m, 1u | ((l - 1) << 8)};
+}
+
 // Pixel subset of the image handled by one call (rectangle or interleaved row stripes).
 struct PixelMap {
   int32_t W, H;
   int32_t stripes;  // 0: rectangle, 1: stripes
   int32_t x0, y0, w, h;
   int32_t srows, sidx, scount;
+  FastDiv frow, fsrows;  // division by the row length (w, or W for stripes) and by srows (set_map_div)
   // 32-bit arithmetic: the host keeps pixel counts below 2^31 (host side: rtx_internal_stripe_rows)
+  // FD = false: the runtime divisions (the same quotients)
+  template <bool FD = true>
   __host__ __device__ __forceinline__ void xy(uint32_t local, int& x, int& y) const {
     if (!stripes) {
-      const uint32_t r = local / (uint32_t)w;
+      const uint32_t r = FD ? frow.div(local) : local / (uint32_t)w;
       x = x0 + (int)(local - r * (uint32_t)w);
       y = y0 + (int)r;
     } else {
-      const int r = (int)(local / (uint32_t)W);
-      x = (int)(local - (uint32_t)r * (uint32_t)W);
-      int blk = r / srows;
-      y = (blk * scount + sidx) * srows + r % srows;
+      const uint32_t r = FD ? frow.div(local) : local / (uint32_t)W;
+      x = (int)(local - r * (uint32_t)W);
+      const uint32_t blk = FD ? fsrows.div(r) : r / (uint32_t)srows;
+      y = ((int)blk * scount + sidx) * srows + (int)(r - blk * (uint32_t)srows);
     }
   }
 };
+inline void set_map_div(PixelMap& m) {
+  const int row = m.stripes ? m.W : m.w;
+  m.frow = make_fastdiv((uint32_t)(row > 1 ? row : 1));
+  m.fsrows = make_fastdiv((uint32_t)(m.srows > 1 ? m.srows : 1));
+}
 
 struct PathQueue {  // SoA, one entry per in-flight path
   double *ox, *oy, *oz, *dx, *dy, *dz, *tx, *ty, *tz;
@@ -72,6 +101,7 @@ struct RenderArgs {
   uint64_t seed;
   int64_t npix;         // pixels in the subset
   int32_t K;            // samples in this group
+  FastDiv fK;           // division by K (set with it: set_group)
   int32_t s0;           // first sample index of the group
   int32_t max_depth;
   int32_t scatter_api;  // megakernel (Scatter/GetPixel) semantics
@@ -472,16 +502,25 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
       if (COUNT && kArgsAtRefill && (Ar.npix != A.npix || Ar.seed != A.seed || Ar.stack_slots != A.stack_slots))
         __builtin_trap();
       // nslots < 2^32 (checked on the host): 32-bit division
+      // the fixed-spp kernel (MAP 0) maps slot -> pixel -> row with the launch-constant divisions
+      // (FastDiv: C2 +0.8 %, C5 +0.6 %, C3 +0.1 %, r10l); the phase kernel keeps the runtime
+      // divisions (its C3 adaptive frame -0.35 % with FastDiv, register allocation; r10m)
+      constexpr bool kFdMap1 = false;
       uint2 e = make_uint2(0u, 0u);
       if (MAP == 1) {  // a phase's slot map, or none: uniform groups (the adaptive first pass)
         const uint2* const sm = (const uint2*)next_slot[8 * 16 + 2];
-        e = sm ? sm[slot] : make_uint2(slot / (uint32_t)Ar.K, (uint32_t)Ar.s0 + slot % (uint32_t)Ar.K);
+        if (sm) {
+          e = sm[slot];
+        } else {
+          const uint32_t q = kFdMap1 ? Ar.fK.div(slot) : slot / (uint32_t)Ar.K;
+          e = make_uint2(q, (uint32_t)Ar.s0 + (slot - q * (uint32_t)Ar.K));
+        }
       }
-      const uint32_t p = MAP ? e.x : (uint32_t)slot / (uint32_t)Ar.K;
+      const uint32_t p = MAP ? e.x : Ar.fK.div(slot);
       if (!(Ar.conv && Ar.conv[p])) {
         const int k = MAP ? 0 : (int)((uint32_t)slot - p * (uint32_t)Ar.K);
         int x, y;
-        Ar.map.xy(p, x, y);
+        Ar.map.template xy<MAP == 0 || kFdMap1>(p, x, y);
         pix = (uint32_t)(y * Ar.map.W + x), smp = MAP ? e.y : (uint32_t)(Ar.s0 + k);
         Rng g = make_rng(A.seed, pix, smp, 0u);
         get_ray<NODOF>(Ar.cam, x, y, g, P.o, P.d);
@@ -521,20 +560,13 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
           trav_globals<COUNT>(A.S, P.o, P.d, tmin, c, trs);
         }
         // parking only when some lane of this round finishes first: every round makes progress
-#ifndef RTX_AB_LEAFMIN_MAP1
-#define RTX_AB_LEAFMIN_MAP1 kLeafSpecMin
-#endif
-#ifndef RTX_AB_PARKAT_MAP1
-#define RTX_AB_PARKAT_MAP1 kParkAt
-#endif
-        constexpr int kLeafMinK = MAP == 1 ? RTX_AB_LEAFMIN_MAP1 : kLeafSpecMin;
-        constexpr int kParkAtK = MAP == 1 ? RTX_AB_PARKAT_MAP1 : kParkAt;
+        // (the phase launches, MAP 1, run the same thresholds: leaf rounds at 6 / 12 lanes and
+        // parking at 12 / 20 lanes measured within noise on C3 adaptive, r10j)
         const bool done =
-            kSpecLds ? trace4_run_spec<STACK, COUNT, TK, decltype(c), kLeafMinK>(A.S, P.o, P.d, tmin, stk16, leafq,
-                                                                                kBlock, c, trs,
-                                                                                active > kParkAtK ? kParkAtK : -1)
+            kSpecLds ? trace4_run_spec<STACK, COUNT, TK>(A.S, P.o, P.d, tmin, stk16, leafq, kBlock, c, trs,
+                                                         active > kParkAt ? kParkAt : -1)
                      : trace4_run<STACK, COUNT, TK>(A.S, P.o, P.d, tmin, stk, kBlock, c, trs,
-                                                    active > kParkAtK ? kParkAtK : -1);
+                                                    active > kParkAt ? kParkAt : -1);
         parked = !done;
         if constexpr (COUNT) c.t_walk = __builtin_amdgcn_s_memtime();
         if (parked) continue;

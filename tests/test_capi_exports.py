@@ -87,3 +87,32 @@ def test_persistent_lds_regions_are_disjoint(rtx_mod, park):
             assert a1 <= b0, (slots, regions)
         assert thr % 8 == 0 and hitp % 8 == 0 and tl % 8 == 0, (slots, thr, hitp, tl)
         assert end <= 160 * 1024, (slots, end)  # a workgroup may take all 160 KiB
+
+
+def test_launch_constant_division_is_exact(rtx_mod):
+    """FastDiv (rtx_kernels.h): the kernels divide slot and pixel indices by launch constants (the
+    group's samples per pixel, the row length, the stripe height) with a multiply-high and two
+    shifts; it must equal the integer division for every 32-bit dividend.  Checked on the host
+    (the same inline code the kernels run) for divisors 1..4096, powers of two and their
+    neighbours to 2^31, and random divisors, against random and boundary dividends."""
+    import ctypes as C
+
+    import numpy as np
+
+    f = rtx_mod.lib().rtx_internal_fastdiv
+    f.argtypes = [C.c_uint32, C.c_void_p, C.c_int64, C.c_void_p]
+    f.restype = C.c_int
+    rng = np.random.default_rng(7)
+    ds = list(range(1, 4097)) + [(1 << k) + e for k in range(12, 32) for e in (-1, 0, 1)]
+    ds += [int(x) for x in rng.integers(4097, 1 << 32, 300)]
+    top = np.uint64((1 << 32) - 1)
+    for d in ds:
+        d = int(min(d, (1 << 32) - 1))
+        n = np.concatenate([rng.integers(0, 1 << 32, 512, dtype=np.uint64),
+                            np.array([0, 1, d - 1, d, d + 1, 2 * d - 1, 2 * d], dtype=np.uint64),
+                            top - np.arange(4, dtype=np.uint64),
+                            (top // np.uint64(d)) * np.uint64(d) - np.arange(2, dtype=np.uint64)])
+        n = np.clip(n, 0, top).astype(np.uint32)
+        out = np.zeros_like(n)
+        assert f(d, n.ctypes.data, len(n), out.ctypes.data) == 0
+        assert np.array_equal(out, n // np.uint32(d)), d
