@@ -395,6 +395,8 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
     // primary-generation code over several lanes.
     const unsigned long long idle = __ballot(!has);
     bool fresh = false;
+    // (re-checked with the cheaper primary setup, FastDiv: PARK at 8 / 10, plain at 16 / 20 idle
+    // lanes within +-0.4 %, r10q)
     constexpr int kRefill = kPark ? kRefillMinPark : kRefillMin;
     if (kShared) {
       // block-shared chunks: the wave takes slots from its own chunk word (an LDS add), then from
