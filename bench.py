@@ -9,7 +9,7 @@ runs from the first ray generation to the framebuffer on the host.
 Workloads (BASELINE.json configs): the default is the north-star scene, the Stanford bunny:
   * 1 GPU:  C3, bunny 1000x562, 200 spp, depth 20, fixed spp
   * N GPUs: C4, bunny 3840x2160, 1024 spp, depth 50, the SAME frame split over the N ranks
-    (strong scaling): the image's rows are interleaved 8-row stripes, stripe k -> rank k mod N
+    (strong scaling): the image's rows are interleaved 4-row stripes, stripe k -> rank k mod N
     (SURVEY §8e); every rank copies its stripes into one shared host framebuffer
     (/dev/shm); no collective touches the data path (a gloo process group carries only the
     timing barrier and the max-over-ranks reduction).
@@ -58,7 +58,7 @@ WORKLOADS = {  # name -> (scene recipe, camera preset, width, spp, depth)
 N_SIMD, CLOCK_HZ = 1024, 2.4e9
 HBM_PEAK_GBS = 8000.0
 L2_SHARED_GBS = 18800.0  # rows shared by every workgroup, served by the XCD's L2 (MI355X_MICROARCH.md)
-STRIPE_ROWS = 8
+STRIPE_ROWS = 4  # interleaved 4-row stripes: max/mean rank load 1.002 at N = 8 for C4 (8 rows: 1.011)
 ADAPTIVE_MIN_SPP, ADAPTIVE_REL = 16, float(np.float32(0.05))  # wavefront.cc:42-43 (kRelThresh is a float)
 
 
