@@ -98,7 +98,6 @@ def main():
         else:
             ops = [o for o in rest.split("//")[0].split(",") if o.strip()]
             plain = operands_plain(ops)
-            short = re.sub(r"_(e32|e64)$", "", mn)
             if b in PAIRABLE and plain:
                 kind = "pairable"
             elif b in PAIRABLE or b in MEASURED_UNPAIRED or b.startswith("v_cmp") or pmc_class(b) != "other" and \
@@ -108,7 +107,6 @@ def main():
                 kind = "unmeasured_vop2"
             else:
                 kind = "unmeasured_other"
-            del short
         c = pmc_class(b)
         for k in ("all",) + (("loop",) if in_loop else ()):
             counts[k][(c, kind)] += 1
