@@ -545,6 +545,11 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
     }
     if constexpr (COUNT) c.t_seg = __builtin_amdgcn_s_memtime();
     if (!has) continue;
+    // wave priority by phase: a wave walking (node visits, leaf tests) outranks one shading or
+    // refilling, so the SIMD's issue slots go first to the walks, whose loads are the long
+    // latencies (C3 +0.9 % over the load barriers alone; shading above walking, or leaf rounds
+    // above or below node visits: slower; profiles/r06/ab/r10z_prio_c3.txt, r11c_c3.txt)
+    __builtin_amdgcn_s_setprio(1);
     // ---- one segment: closest hit + shading ----
     V3 L;
     bool cont;
@@ -585,6 +590,7 @@ __global__ __launch_bounds__(kBlock, kTraceWaves) void k_persistent(RenderArgs A
         const unsigned long long sh = __ballot(1);
         if ((int)lane_id() == __ffsll((long long)sh) - 1) c.wshade++, c.lshade += (uint32_t)__popcll(sh);
       }
+      __builtin_amdgcn_s_setprio(0);  // shading (and the refill after it) at the base priority
       Hit h;
       rtx_material m;
       if (best >= 0) finish_hit_at<false>(A.S, best, tb, P.o, P.d, h);
